@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""bench.py — QP solves/s of the f110qp HIP path (BASELINE.json metric) on 1..8 MI355X.
+
+A "step" is one f110qp_solve_batch_dev launch over one batch of synthetic ticks already
+resident in HBM (linearise + condense + exact QP solve + (u*, x*) write-back for every QP).
+Default workload: BASELINE.json configs[1] = 1,024 independent horizon-20 QPs, box input
+constraints. One process per GPU (torch.distributed, RCCL backend); each rank solves its own
+batch (weak scaling, no data-path collective: the QPs are independent); the timed region is
+bracketed by barrier + synchronize and the max over ranks is reported.
+
+Extra JSON fields: "roofline" (dominant kernel = the solve kernel: algorithmic bytes and
+flops per launch / its average duration from HIP events on the launch stream) and
+"cpu_baseline" (the CPU oracle timed on a bounded sample on the host cores; rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "f110-mpc_amd"))
+
+CONFIGS = {
+    # name: (batch per GPU, horizon, gap rows active, description)
+    "c2": (1024, 20, False, "configs[1]: batch=1024 QPs, horizon=20, box constraints only"),
+    "c3": (4096, 20, True, "configs[2]: batch=4096 QPs, horizon=20, + half-space gap constraints"),
+    "c2_big": (65536, 20, False, "throughput: batch=65536 QPs, horizon=20, box constraints"),
+}
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
+
+
+def bytes_per_qp(N: int, gap: bool) -> int:
+    """ABI bytes moved per QP: x0, u_lin, x_ref (+ halfspace) in; u*, x*, status, iters out."""
+    inp = 4 * (3 + 2 + 3 * N + (6 if gap else 0))
+    out = 4 * (2 * N + 3 * (N + 1) + 1 + 1)
+    return inp + out
+
+
+def flops_per_qp(N: int, mean_iters: float, mean_active: float) -> float:
+    """Algorithmic flops of the kernel's algorithm (DESIGN.md "Roofline"):
+    closed-form Hessian 25 n^2, symmetric sweep inverse 2 n^3, x = -W g 2 n^2,
+    per active-set iteration 2 n (W n_p) + 2 q^2 (two triangular solves) + 2 n q (z),
+    two fp64 refinement steps 2 (2 n^2 + 2 q^2 + 2 n q); n = 2N."""
+    n = 2 * N
+    q = mean_active
+    return 25 * n * n + 2 * n ** 3 + 2 * n * n + mean_iters * (2 * n + 2 * q * q + 2 * n * q) \
+        + 2 * (2 * n * n + 2 * q * q + 2 * n * q)
+
+
+def load_traffic(config: str):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int):
+    """Time the CPU oracle (exact condensed QP solve, fp64, OpenMP) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker only: used here for the cpu_baseline leg, never for the GPU value
+    from f110qp import workload
+
+    B = 4096
+    w = workload.make_batch(B, N, seed=12345)
+    hs = None
+    if gap:
+        hs = _halfspaces_host(w, B)
+    prm = oracle.params(N)
+    oracle.solve_batch(prm, w["x0"][:64], w["u_lin"][:64], w["x_ref"][:64], hs if hs is None else hs[:64],
+                       gap_active=gap, num_threads=threads)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.solve_batch(prm, w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=gap, num_threads=threads)
+        n += B
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return dict(value=n / el, unit="QP solves/s", cores=threads, kind="port",
+                sample=f"{n} QPs ({n // B} x {B} {config} ticks, horizon {N}) in {el:.1f} s: oracle/"
+                       f"f110_oracle.c exact dual active-set (fp64) with OpenMP over QPs")
+
+
+def _halfspaces_host(w, B):
+    from f110qp import capi, workload
+
+    ranges, amin, ainc, amax = workload.make_scans(B, seed=99)
+    hs = np.zeros((B, 2, 3), np.float32)
+    for b in range(B):
+        l1, l2 = capi.find_half_spaces(w["x0"][b].astype(np.float64), ranges[b], amin, ainc, amax)
+        hs[b, 0] = l1
+        hs[b, 1] = l2
+    return hs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="override batch per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from f110qp import capi, workload
+
+    Bper, N, gap, desc = CONFIGS[args.config]
+    if args.batch:
+        Bper = args.batch
+    w = workload.make_batch(Bper, N, seed=1000 + rank)
+    x0 = torch.from_numpy(w["x0"]).to(dev)
+    ul = torch.from_numpy(w["u_lin"]).to(dev)
+    xr = torch.from_numpy(w["x_ref"]).to(dev)
+    hs = None
+    if gap:
+        ranges, amin, ainc, amax = workload.make_scans(Bper, seed=2000 + rank)
+        hs = torch.empty((Bper, 2, 3), dtype=torch.float32, device=dev)
+        capi.find_half_spaces_dev(x0, torch.from_numpy(ranges).to(dev), amin, ainc, amax, hs)
+    uo = torch.empty((Bper, N, 2), dtype=torch.float32, device=dev)
+    xo = torch.empty((Bper, N + 1, 3), dtype=torch.float32, device=dev)
+    st = torch.empty((Bper,), dtype=torch.int32, device=dev)
+    it = torch.empty((Bper,), dtype=torch.int32, device=dev)
+    cfg = capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, device=dev.index)
+    solver = capi.Solver(cfg)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        solver.solve_dev(x0, ul, xr, hs, uo, xo, st, it, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # solver statistics of the last step (all steps solve the same batch)
+    stn = st.cpu().numpy()
+    itn = it.cpu().numpy()
+    solved = float((stn == capi.SOLVED).mean())
+
+    # dominant kernel duration: HIP events around single launches on the launch stream
+    evs = []
+    for _ in range(20):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        step()
+        b.record(stream)
+        evs.append((a, b))
+    torch.cuda.synchronize(dev)
+    kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))  # ms per launch
+
+    total_qps = Bper * world * args.steps
+    value = total_qps / el
+    ms_per_step = el / args.steps * 1e3
+    bpq = bytes_per_qp(N, gap)
+    # active-set size ~ iterations for an add-only run; use iterations as the upper bound
+    fpq = flops_per_qp(N, float(itn.mean()), float(itn.mean()))
+    achieved_gbs = bpq * Bper / (kms * 1e-3) / 1e9
+    achieved_tf = fpq * Bper / (kms * 1e-3) / 1e12
+    traffic = load_traffic(args.config)
+
+    out = {
+        "metric": "QP solves/s (horizon=20, nx=3 reference model, nu=2)",
+        "value": value,
+        "unit": "QP solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 (fp64 refinement)",
+        "data": "synthetic (seeded; SURVEY.md 8(d) recipe: simulate_dynamics mini paths)",
+        "config": {
+            "workload": desc,
+            "batch_per_gpu": Bper,
+            "global_batch": Bper * world,
+            "horizon": N,
+            "gap_rows": bool(gap),
+            "parallelism": f"independent QP shards x{world} (no collective)",
+            "solved_fraction": solved,
+            "mean_active_set_iters": float(itn.mean()),
+            "max_active_set_iters": int(itn.max()),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "f110qp::solve_kernel",
+            "kernel_ms_per_launch": kms,
+            "algorithmic_bytes_per_qp": bpq,
+            "fp32_compute": {"achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                             "frac": achieved_tf / FP32_PEAK_TFLOPS, "flops_per_qp": fpq},
+            "note": "latency-bound (serial active-set chain per wave); neither HBM nor FP32 peak binds",
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.config, N, gap, args.cpu_seconds, args.cpu_threads)
+        except Exception as e:  # the baseline must never take the GPU number down
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    solver.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

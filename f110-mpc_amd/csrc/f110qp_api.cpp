@@ -1,0 +1,270 @@
+// f110qp_api.cpp — the C ABI (include/f110qp.h) over the gfx950 kernels.
+//
+// Host-side responsibilities only: argument validation, the device workspace of a context,
+// H2D/D2H for the host-pointer entry points, and Constraints::FindHalfSpaces for one scan
+// (reference src/constraints.cpp:116-265) for callers that hold a single LaserScan.
+// No C++ exception crosses this boundary.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "f110qp.h"
+#include "f110qp_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error = "";
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(F110QP_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Device buffer that only grows.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+}  // namespace
+
+struct f110qp_ctx {
+  f110qp_config cfg;
+  f110qp::KParams kp;
+  DevBuf x0, ul, xr, hs, uo, xo, st, it;
+  hipStream_t stream = nullptr;
+};
+
+extern "C" {
+
+int f110qp_version(void) { return F110QP_API_VERSION; }
+
+const char* f110qp_last_error(void) { return g_last_error.c_str(); }
+
+void f110qp_default_config(f110qp_config* c, int horizon) {
+  if (!c) return;
+  std::memset(c, 0, sizeof(*c));
+  c->horizon = horizon;  // params.yaml:12 (reference default 30)
+  c->dt = 0.01f;         // params.yaml:13
+  c->q[0] = 10.0; c->q[1] = 10.0; c->q[2] = 0.0;  // params.yaml:1-3
+  c->r[0] = 0.10; c->r[1] = 5.0;                  // params.yaml:5-6
+  c->u_des[0] = 4.5; c->u_des[1] = 0.0;           // params.yaml:42-43
+  c->u_min[0] = 3.0f; c->u_min[1] = -0.43f;       // params.yaml:47, constraints.cpp:21
+  c->u_max[0] = 4.5f; c->u_max[1] = 0.43f;        // params.yaml:46, constraints.cpp:19
+  c->gap_mode = F110QP_GAP_INACTIVE;
+  c->max_iter = 0;
+  c->device = 0;
+}
+
+static int validate_config(const f110qp_config* c) {
+  if (!c) return fail(F110QP_ERR_INVALID, "config is NULL");
+  if (c->horizon < 1 || c->horizon > 32)
+    return fail(F110QP_ERR_INVALID, "horizon must be in [1, 32] (one wave holds 2N inputs)");
+  if (!(c->dt > 0.f) || !std::isfinite(c->dt)) return fail(F110QP_ERR_INVALID, "dt must be > 0");
+  for (int i = 0; i < 3; i++)
+    if (!(c->q[i] >= 0.0)) return fail(F110QP_ERR_INVALID, "Q must be >= 0");
+  for (int i = 0; i < 2; i++) {
+    if (!(c->r[i] > 0.0)) return fail(F110QP_ERR_INVALID, "R must be > 0 (strictly convex QP)");
+    if (!(c->u_min[i] <= c->u_max[i])) return fail(F110QP_ERR_INVALID, "u_min > u_max");
+  }
+  if (c->gap_mode != F110QP_GAP_INACTIVE && c->gap_mode != F110QP_GAP_ACTIVE)
+    return fail(F110QP_ERR_INVALID, "gap_mode must be F110QP_GAP_INACTIVE or F110QP_GAP_ACTIVE");
+  if (c->max_iter < 0) return fail(F110QP_ERR_INVALID, "max_iter must be >= 0");
+  return F110QP_OK;
+}
+
+int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
+  if (!out) return fail(F110QP_ERR_INVALID, "ctx out-pointer is NULL");
+  *out = nullptr;
+  int rc = validate_config(cfg);
+  if (rc) return rc;
+  f110qp_ctx* c = new (std::nothrow) f110qp_ctx();
+  if (!c) return fail(F110QP_ERR_ALLOC, "out of host memory");
+  c->cfg = *cfg;
+  f110qp::KParams& k = c->kp;
+  k.N = cfg->horizon;
+  k.dt = cfg->dt;
+  for (int i = 0; i < 3; i++) k.q[i] = cfg->q[i];
+  for (int i = 0; i < 2; i++) {
+    k.r[i] = cfg->r[i];
+    k.udes[i] = cfg->u_des[i];
+    k.umin[i] = cfg->u_min[i];
+    k.umax[i] = cfg->u_max[i];
+  }
+  const int nu = 2 * cfg->horizon;
+  k.max_iter = cfg->max_iter > 0 ? cfg->max_iter : 8 * (nu + (cfg->gap_mode ? nu : 0)) + 16;
+  *out = c;
+  return F110QP_OK;
+}
+
+void f110qp_destroy(f110qp_ctx* c) {
+  if (!c) return;
+  c->x0.release(); c->ul.release(); c->xr.release(); c->hs.release();
+  c->uo.release(); c->xo.release(); c->st.release(); c->it.release();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+static int check_batch_args(f110qp_ctx* c, int batch, const void* x0, const void* ul,
+                            const void* xr, const void* hs, const void* uo, const void* xo,
+                            const void* st) {
+  if (!c) return fail(F110QP_ERR_INVALID, "ctx is NULL");
+  if (batch < 0) return fail(F110QP_ERR_INVALID, "batch < 0");
+  if (batch == 0) return F110QP_OK;
+  if (!x0 || !ul || !xr || !uo || !xo || !st)
+    return fail(F110QP_ERR_INVALID, "x0/u_lin/x_ref/u_out/x_out/status must be non-NULL");
+  if (c->cfg.gap_mode == F110QP_GAP_ACTIVE && !hs)
+    return fail(F110QP_ERR_INVALID, "gap_mode ACTIVE needs the halfspace array");
+  if (batch > (1 << 30) / 64) return fail(F110QP_ERR_INVALID, "batch too large");
+  return F110QP_OK;
+}
+
+int f110qp_solve_batch_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                           const float* xr, const float* hs, float* uo, float* xo, int* st,
+                           int* it, void* stream) {
+  int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
+  if (rc || batch == 0) return rc;
+  const float* h = (c->cfg.gap_mode == F110QP_GAP_ACTIVE) ? hs : nullptr;
+  hipError_t e = f110qp::launch_solve(c->kp, batch, x0, ul, xr, h, uo, xo, st, it,
+                                      (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
+  return F110QP_OK;
+}
+
+int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                       const float* xr, const float* hs, float* uo, float* xo, int* st,
+                       int* it) {
+  int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
+  if (rc || batch == 0) return rc;
+  hipError_t e = hipSetDevice(c->cfg.device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if (!c->stream) {
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+  }
+  const int N = c->cfg.horizon;
+  const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
+  const size_t B = (size_t)batch;
+  const size_t s_x0 = B * 3 * 4, s_ul = B * 2 * 4, s_xr = B * N * 3 * 4, s_hs = B * 6 * 4;
+  const size_t s_uo = B * N * 2 * 4, s_xo = B * (N + 1) * 3 * 4, s_st = B * 4;
+  if ((e = c->x0.ensure(s_x0)) || (e = c->ul.ensure(s_ul)) || (e = c->xr.ensure(s_xr)) ||
+      (gap && (e = c->hs.ensure(s_hs))) || (e = c->uo.ensure(s_uo)) || (e = c->xo.ensure(s_xo)) ||
+      (e = c->st.ensure(s_st)) || (e = c->it.ensure(s_st)))
+    return hip_fail(e, "hipMalloc workspace");
+  hipStream_t s = c->stream;
+  if ((e = hipMemcpyAsync(c->x0.p, x0, s_x0, hipMemcpyHostToDevice, s)) ||
+      (e = hipMemcpyAsync(c->ul.p, ul, s_ul, hipMemcpyHostToDevice, s)) ||
+      (e = hipMemcpyAsync(c->xr.p, xr, s_xr, hipMemcpyHostToDevice, s)) ||
+      (gap && (e = hipMemcpyAsync(c->hs.p, hs, s_hs, hipMemcpyHostToDevice, s))))
+    return hip_fail(e, "hipMemcpyAsync H2D");
+  e = f110qp::launch_solve(c->kp, batch, (const float*)c->x0.p, (const float*)c->ul.p,
+                           (const float*)c->xr.p, gap ? (const float*)c->hs.p : nullptr,
+                           (float*)c->uo.p, (float*)c->xo.p, (int*)c->st.p, (int*)c->it.p, s);
+  if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
+  if ((e = hipMemcpyAsync(uo, c->uo.p, s_uo, hipMemcpyDeviceToHost, s)) ||
+      (e = hipMemcpyAsync(xo, c->xo.p, s_xo, hipMemcpyDeviceToHost, s)) ||
+      (e = hipMemcpyAsync(st, c->st.p, s_st, hipMemcpyDeviceToHost, s)) ||
+      (it && (e = hipMemcpyAsync(it, c->it.p, s_st, hipMemcpyDeviceToHost, s))))
+    return hip_fail(e, "hipMemcpyAsync D2H");
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  return F110QP_OK;
+}
+
+int f110qp_condense_debug_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                              const float* xr, double* H, double* g, void* stream) {
+  if (!c) return fail(F110QP_ERR_INVALID, "ctx is NULL");
+  if (batch < 0) return fail(F110QP_ERR_INVALID, "batch < 0");
+  if (batch == 0) return F110QP_OK;
+  if (!x0 || !ul || !xr || !H || !g) return fail(F110QP_ERR_INVALID, "NULL pointer argument");
+  hipError_t e = f110qp::launch_condense_debug(c->kp, batch, x0, ul, xr, H, g,
+                                               (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "condense kernel launch");
+  return F110QP_OK;
+}
+
+// Constraints::FindHalfSpaces (src/constraints.cpp:116-265) for one scan, host code with the
+// reference's float32 member types; the ROS marker publish (:191-229) is not reproduced.
+int f110qp_find_half_spaces(const double state[3], const float* ranges, int nr, float angle_min,
+                            float angle_inc, float angle_max, float ftg_thresh, float divider,
+                            float buffer, double l1[3], double l2[3]) {
+  if (!state || !ranges || !l1 || !l2 || nr <= 0)
+    return fail(F110QP_ERR_INVALID, "NULL pointer or empty scan");
+  int num_scans = (int)((angle_max - angle_min) / angle_inc + 1);
+  if (num_scans > nr) num_scans = nr;
+  int max_gap = -1, best_lo = 0, best_hi = 0, lo = -1, hi = -1;
+  bool in_gap = false;
+  const float lim = 1.571f / divider;
+  for (int ii = 0; ii < num_scans; ii++) {
+    const float angle = angle_min + ii * angle_inc;
+    if (angle > -lim && angle < lim) {
+      if (ranges[ii] > ftg_thresh) {
+        if (in_gap) hi = ii;
+        else { lo = ii; in_gap = true; }
+      } else {
+        in_gap = false;
+      }
+      if (hi - lo > max_gap) { max_gap = hi - lo; best_hi = hi; best_lo = lo; }
+    }
+  }
+  if (best_hi - best_lo > 2 * buffer) {
+    best_hi = (int)(best_hi - buffer);
+    best_lo = (int)(best_lo + buffer);
+  }
+  if (best_lo < 0 || best_hi < 0 || best_lo >= nr || best_hi >= nr)
+    return fail(F110QP_ERR_INVALID, "scan holds no gap (reference reads ranges[-1] here)");
+  const double poseX = state[0], poseY = state[1];
+  const float cur = (float)state[2];
+  const float ang1 = angle_min + best_lo * angle_inc + cur;
+  const float ang2 = angle_min + best_hi * angle_inc + cur;
+  const float p1x = (float)(ranges[best_lo] * std::cos((double)ang1) + poseX);
+  const float p1y = (float)(ranges[best_lo] * std::sin((double)ang1) + poseY);
+  const float p2x = (float)(ranges[best_hi] * std::cos((double)ang2) + poseX);
+  const float p2y = (float)(ranges[best_hi] * std::sin((double)ang2) + poseY);
+  const float px = (float)poseX, py = (float)poseY;
+  float a1 = py - p1y, b1 = p1x - px, c1 = px * p1y - py * p1x;
+  if (a1 * p2x + b1 * p2y + c1 < 0) { a1 = -a1; b1 = -b1; c1 = -c1; }
+  float a2 = py - p2y, b2 = p2x - px, c2 = px * p2y - py * p2x;
+  if (a2 * p1x + b2 * p1y + c2 < 0) { a2 = -a2; b2 = -b2; c2 = -c2; }
+  l1[0] = a1; l1[1] = b1; l1[2] = (double)c1 + 0.5;
+  l2[0] = a2; l2[1] = b2; l2[2] = (double)c2 + 0.5;
+  return F110QP_OK;
+}
+
+int f110qp_find_half_spaces_dev(int batch, const float* states, const float* ranges, int nr,
+                                float angle_min, float angle_inc, float angle_max,
+                                float ftg_thresh, float divider, float buffer, float* hs,
+                                int* gap_lo, int* gap_hi, void* stream) {
+  if (batch < 0 || nr <= 0) return fail(F110QP_ERR_INVALID, "bad batch / num_ranges");
+  if (batch == 0) return F110QP_OK;
+  if (!states || !ranges || !hs) return fail(F110QP_ERR_INVALID, "NULL pointer argument");
+  hipError_t e = f110qp::launch_half_spaces(batch, states, ranges, nr, angle_min, angle_inc,
+                                            angle_max, ftg_thresh, divider, buffer, hs, gap_lo,
+                                            gap_hi, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "half-space kernel launch");
+  return F110QP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,41 @@
+// f110qp_kernels.h — internal launch interface between the C ABI (f110qp_api.cpp) and the
+// gfx950 kernels (f110qp_kernels.hip, halfspace_kernels.hip). Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace f110qp {
+
+// per-QP status ids (== F110QP_* in include/f110qp.h)
+constexpr int F110QP_SOLVED_ID = 1;
+constexpr int F110QP_MAX_ITER_ID = -2;
+constexpr int F110QP_PRIMAL_INFEASIBLE_ID = -3;
+constexpr int F110QP_NUMERICAL_ID = -10;
+
+// Kernel-side copy of f110qp_config (passed by value in kernarg memory).
+struct KParams {
+  int N;          // horizon
+  float dt;       // MPC::dt_ (float)
+  double q[3];    // diag Q
+  double r[2];    // diag R
+  double udes[2]; // desired input
+  float umin[2];  // input lower bounds
+  float umax[2];  // input upper bounds
+  int max_iter;   // active-set iteration cap
+};
+
+// Solve B QPs. hs == nullptr -> box-only kernel (gap rows inactive).
+hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u_lin,
+                        const float* x_ref, const float* hs, float* u_out, float* x_out,
+                        int* status, int* iters, hipStream_t stream);
+
+// Dump the condensed H (B x 2N x 2N) and g (B x 2N) as built by the solve kernel.
+hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* u_lin,
+                                 const float* x_ref, double* H, double* g, hipStream_t stream);
+
+// Batched FindHalfSpaces (constraints.cpp:116-265), one wave per scan.
+hipError_t launch_half_spaces(int B, const float* states, const float* ranges, int num_ranges,
+                              float angle_min, float angle_inc, float angle_max, float thresh,
+                              float divider, float buffer, float* hs, int* gap_lo, int* gap_hi,
+                              hipStream_t stream);
+
+}  // namespace f110qp

@@ -1,0 +1,217 @@
+"""ctypes binding of libf110qp.so (include/f110qp.h).
+
+This is the Python-side binding a maintainer would write over the C ABI; the product's
+compute path is the HIP kernel behind it. There is no CPU fallback: if the library is
+missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libf110qp.so")
+
+OK = 0
+ERR_INVALID = -1
+ERR_HIP = -2
+ERR_ALLOC = -3
+SOLVED = 1
+MAX_ITER = -2
+PRIMAL_INFEASIBLE = -3
+NUMERICAL = -10
+GAP_INACTIVE = 0
+GAP_ACTIVE = 1
+MAX_HORIZON = 64
+
+# every symbol include/f110qp.h declares
+EXPORTED = (
+    "f110qp_version",
+    "f110qp_last_error",
+    "f110qp_default_config",
+    "f110qp_create",
+    "f110qp_destroy",
+    "f110qp_solve_batch",
+    "f110qp_solve_batch_dev",
+    "f110qp_condense_debug_dev",
+    "f110qp_find_half_spaces",
+    "f110qp_find_half_spaces_dev",
+)
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("horizon", C.c_int),
+        ("dt", C.c_float),
+        ("q", C.c_double * 3),
+        ("r", C.c_double * 2),
+        ("u_des", C.c_double * 2),
+        ("u_min", C.c_float * 2),
+        ("u_max", C.c_float * 2),
+        ("gap_mode", C.c_int),
+        ("max_iter", C.c_int),
+        ("device", C.c_int),
+    ]
+
+
+class F110QPError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libf110qp.so (raises if it is missing: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise F110QPError(f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` (hipcc, gfx950)")
+    L = C.CDLL(LIB_PATH)
+    fp = C.c_void_p
+    L.f110qp_version.restype = C.c_int
+    L.f110qp_last_error.restype = C.c_char_p
+    L.f110qp_default_config.argtypes = [C.POINTER(Config), C.c_int]
+    L.f110qp_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(Config)]
+    L.f110qp_destroy.argtypes = [C.c_void_p]
+    L.f110qp_solve_batch.argtypes = [C.c_void_p, C.c_int] + [fp] * 8
+    L.f110qp_solve_batch_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 9
+    L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
+    L.f110qp_find_half_spaces.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_float), C.c_int,
+                                          C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
+                                          C.c_float, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.f110qp_find_half_spaces_dev.argtypes = [C.c_int, fp, fp, C.c_int, C.c_float, C.c_float, C.c_float,
+                                              C.c_float, C.c_float, C.c_float, fp, fp, fp, fp]
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return load().f110qp_last_error().decode()
+
+
+def _check(rc: int, what: str):
+    if rc != OK:
+        raise F110QPError(f"{what} failed ({rc}): {last_error()}")
+
+
+def default_config(horizon: int, **over) -> Config:
+    c = Config()
+    load().f110qp_default_config(C.byref(c), horizon)
+    for k, v in over.items():
+        if k in ("q", "r", "u_des", "u_min", "u_max"):
+            arr = getattr(c, k)
+            for i, x in enumerate(v):
+                arr[i] = x
+        else:
+            setattr(c, k, v)
+    return c
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+def _tp(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class Solver:
+    """One f110qp context (device workspace). Mirrors the reference's OsqpEigen::Solver
+    member of MPC (include/f110-mpc/mpc.h:63) for B instances at once."""
+
+    def __init__(self, config: Config):
+        self.lib = load()
+        self.config = config
+        h = C.c_void_p()
+        _check(self.lib.f110qp_create(C.byref(h), C.byref(config)), "f110qp_create")
+        self._h = h
+
+    @property
+    def horizon(self) -> int:
+        return self.config.horizon
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.f110qp_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, x0, u_lin, x_ref, halfspace=None):
+        """Host arrays in, host arrays out (synchronous). Returns (u[B,N,2], x[B,N+1,3],
+        status[B], iters[B])."""
+        N = self.horizon
+        x0 = np.ascontiguousarray(x0, np.float32).reshape(-1, 3)
+        B = x0.shape[0]
+        ul = np.ascontiguousarray(u_lin, np.float32).reshape(B, 2)
+        xr = np.ascontiguousarray(x_ref, np.float32).reshape(B, N, 3)
+        hs = None if halfspace is None else np.ascontiguousarray(halfspace, np.float32).reshape(B, 6)
+        u = np.empty((B, N, 2), np.float32)
+        x = np.empty((B, N + 1, 3), np.float32)
+        st = np.empty(B, np.int32)
+        it = np.empty(B, np.int32)
+        _check(self.lib.f110qp_solve_batch(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(u), _p(x),
+                                           _p(st), _p(it)), "f110qp_solve_batch")
+        return u, x, st, it
+
+    def solve_dev(self, x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters=None, stream=None):
+        """Device (torch) tensors in/out, enqueued on `stream` (torch.cuda stream or None =
+        current stream). Asynchronous."""
+        import torch
+
+        B = x0.shape[0]
+        if stream is None:
+            stream = torch.cuda.current_stream(x0.device)
+        _check(self.lib.f110qp_solve_batch_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
+                                               _tp(u_out), _tp(x_out), _tp(status), _tp(iters),
+                                               C.c_void_p(stream.cuda_stream)), "f110qp_solve_batch_dev")
+
+    def condense_debug_dev(self, x0, u_lin, x_ref, H_out, g_out, stream=None):
+        import torch
+
+        B = x0.shape[0]
+        if stream is None:
+            stream = torch.cuda.current_stream(x0.device)
+        _check(self.lib.f110qp_condense_debug_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(H_out),
+                                                  _tp(g_out), C.c_void_p(stream.cuda_stream)),
+               "f110qp_condense_debug_dev")
+
+
+def find_half_spaces(state, ranges, angle_min, angle_inc, angle_max, thresh=3.0, divider=1.5, buffer=3.0):
+    """Constraints::FindHalfSpaces for one scan (host). Returns (l1, l2) or raises when the
+    scan has no gap."""
+    L = load()
+    s = np.ascontiguousarray(state, np.float64)
+    r = np.ascontiguousarray(ranges, np.float32)
+    l1 = np.zeros(3)
+    l2 = np.zeros(3)
+    rc = L.f110qp_find_half_spaces(s.ctypes.data_as(C.POINTER(C.c_double)), r.ctypes.data_as(C.POINTER(C.c_float)),
+                                   len(r), float(angle_min), float(angle_inc), float(angle_max), float(thresh),
+                                   float(divider), float(buffer), l1.ctypes.data_as(C.POINTER(C.c_double)),
+                                   l2.ctypes.data_as(C.POINTER(C.c_double)))
+    _check(rc, "f110qp_find_half_spaces")
+    return l1, l2
+
+
+def find_half_spaces_dev(states, ranges, angle_min, angle_inc, angle_max, hs_out, gap_lo=None, gap_hi=None,
+                         thresh=3.0, divider=1.5, buffer=3.0, stream=None):
+    """Batched FindHalfSpaces on torch device tensors: states [B,3] f32, ranges [B,R] f32 ->
+    hs_out [B,2,3] f32."""
+    import torch
+
+    L = load()
+    if stream is None:
+        stream = torch.cuda.current_stream(states.device)
+    B, R = ranges.shape
+    _check(L.f110qp_find_half_spaces_dev(B, _tp(states), _tp(ranges), R, float(angle_min), float(angle_inc),
+                                         float(angle_max), float(thresh), float(divider), float(buffer),
+                                         _tp(hs_out), _tp(gap_lo), _tp(gap_hi), C.c_void_p(stream.cuda_stream)),
+           "f110qp_find_half_spaces_dev")

@@ -1,0 +1,112 @@
+"""Synthetic tick batches for the f110qp hot path, numpy only.
+
+The reference ships no datasets; its inputs come from the simulator. The generator follows
+the reference's own recipe for a candidate trajectory:
+  - mini paths: Traj_Plan::generate_traj_table (src/trajectory_planner.cpp:26-72), i.e.
+    `traj_discrete`=50 states from (0,0,0) by Model::simulate_dynamics (src/model.cpp:61-75,
+    CAR_LENGTH = 0.35) at constant speed and steer, dt = 0.01;
+  - car -> world with Transforms::CarPointToWorldPoint (src/transforms.cpp:3-20), as float;
+  - ori = 0 for every reference state (src/project.cpp:147), or the true heading;
+  - u_lin = (4.5, steer): v is forced to 4.5 before MPC::Update (src/project.cpp:170);
+  - half spaces from FindHalfSpaces on a synthetic 1080-beam scan with one guaranteed gap.
+All arrays are in the include/f110qp.h layouts (float32, row-major).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+CAR_LENGTH = 0.35  # src/model.cpp:2
+TRAJ_POINTS = 50   # params.yaml:57 traj_discrete
+SPEED = 4.5        # params.yaml:46 umax; project.cpp:170
+
+
+def mini_paths(steer, speed=SPEED, dt=0.01, points=TRAJ_POINTS):
+    """Vectorised generate_traj_table rollouts: steer [B] -> car-frame states [B, points, 3]."""
+    steer = np.asarray(steer, np.float64).reshape(-1)
+    B = steer.shape[0]
+    out = np.zeros((B, points, 3))
+    s = np.zeros((B, 3))
+    for k in range(1, points):  # trajectory_planner.cpp:291-297
+        d0 = speed * np.cos(s[:, 2])
+        d1 = speed * np.sin(s[:, 2])
+        d2 = np.tan(steer) * speed / CAR_LENGTH
+        s = s + np.stack([d0, d1, d2], 1) * dt
+        out[:, k] = s
+    return out
+
+
+def car_to_world(px, py, pose):
+    """CarPointToWorldPoint: rotate by the pose yaw, add the (float) position -> float32."""
+    th = pose[:, 2:3].astype(np.float64)
+    c, s = np.cos(th), np.sin(th)
+    wx = c * px - s * py + pose[:, 0:1].astype(np.float32).astype(np.float64)
+    wy = s * px + c * py + pose[:, 1:2].astype(np.float32).astype(np.float64)
+    return wx.astype(np.float32), wy.astype(np.float32)
+
+
+def make_batch(batch: int, horizon: int, seed: int = 0, heading: str = "zero", lateral: float = 0.3,
+               steer_range: float = 0.4):
+    """Independent ticks (configs C2/C3 of BASELINE.json). Returns dict(x0, u_lin, x_ref)."""
+    rng = np.random.default_rng(seed)
+    x0 = np.stack([rng.uniform(-50, 50, batch), rng.uniform(-50, 50, batch),
+                   rng.uniform(-np.pi, np.pi, batch)], 1).astype(np.float32)
+    u_lin = np.stack([np.full(batch, SPEED), rng.uniform(-steer_range, steer_range, batch)], 1).astype(np.float32)
+    steer = rng.uniform(-steer_range, steer_range, batch)
+    off = rng.uniform(-lateral, lateral, batch)
+    path = mini_paths(steer)
+    x_ref = _to_ref(path, off, x0, horizon, heading)
+    return dict(x0=x0, u_lin=u_lin, x_ref=x_ref)
+
+
+def _to_ref(path, off, x0, horizon, heading):
+    px = path[:, :horizon, 0]
+    py = path[:, :horizon, 1] + off[:, None]
+    wx, wy = car_to_world(px, py, x0)
+    if heading == "zero":
+        ori = np.zeros_like(wx)
+    else:
+        ori = (x0[:, 2:3].astype(np.float64) + path[:, :horizon, 2]).astype(np.float32)
+    return np.ascontiguousarray(np.stack([wx, wy, ori], 2), np.float32)
+
+
+def make_grouped_batch(scenarios: int, horizon: int, seed: int = 0, lanes=(0.0, 0.25, -0.25, 0.5, -0.5, 0.75),
+                       steers: int = 20, steer_range: float = 0.4, heading: str = "zero"):
+    """Config C4: per scenario one car state and linearisation point shared by
+    len(lanes) x steers candidate mini paths (lateral lane offset x steer value)."""
+    rng = np.random.default_rng(seed)
+    G = len(lanes) * steers
+    x0s = np.stack([rng.uniform(-50, 50, scenarios), rng.uniform(-50, 50, scenarios),
+                    rng.uniform(-np.pi, np.pi, scenarios)], 1).astype(np.float32)
+    uls = np.stack([np.full(scenarios, SPEED), rng.uniform(-steer_range, steer_range, scenarios)], 1).astype(np.float32)
+    steer_vals = np.linspace(-steer_range, steer_range, steers)
+    st = np.tile(steer_vals, len(lanes))
+    off = np.repeat(np.asarray(lanes, np.float64), steers)
+    path = mini_paths(st)
+    x0 = np.repeat(x0s, G, 0)
+    u_lin = np.repeat(uls, G, 0)
+    x_ref = _to_ref(np.tile(path, (scenarios, 1, 1)), np.tile(off, scenarios), x0, horizon, heading)
+    return dict(x0=x0, u_lin=u_lin, x_ref=x_ref, group_size=G)
+
+
+SCAN_BEAMS = 1080
+
+
+def scan_geometry(beams: int = SCAN_BEAMS):
+    amin = np.float32(-np.pi)
+    ainc = np.float32(2 * np.pi / beams)
+    amax = np.float32(amin + ainc * (beams - 1))
+    return amin, ainc, amax
+
+
+def make_scans(batch: int, seed: int = 0, beams: int = SCAN_BEAMS, gap_center=0.6, gap_width=(0.3, 0.9)):
+    """Synthetic LaserScans: short returns (1-2.5 m, below follow_gap_thresh = 3,
+    params.yaml:49) everywhere except one arc of long returns (4-10 m) near the heading."""
+    rng = np.random.default_rng(seed + 7919)
+    amin, ainc, amax = scan_geometry(beams)
+    ang = amin + ainc * np.arange(beams, dtype=np.float64)
+    r = rng.uniform(1.0, 2.5, (batch, beams)).astype(np.float32)
+    ctr = rng.uniform(-gap_center, gap_center, batch)
+    w = rng.uniform(gap_width[0], gap_width[1], batch)
+    m = np.abs(ang[None, :] - ctr[:, None]) < (w[:, None] / 2)
+    r[m] = rng.uniform(4.0, 10.0, int(m.sum())).astype(np.float32)
+    return r, amin, ainc, amax

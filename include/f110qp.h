@@ -1,0 +1,129 @@
+/*
+ * f110qp.h — C ABI of the MI355X batched MPC/QP solver for the f110-mpc control tick.
+ *
+ * Drop-in boundary. In the reference the per-tick hot path is
+ *   MPC::Update (src/mpc.cpp:69-143)
+ *     Model::Linearize            (src/model.cpp:30-59)
+ *     Constraints::FindHalfSpaces (src/constraints.cpp:116-265)
+ *     MPC::CreateGradientVector / Update{LinearConstraintMatrix,Lower,Upper}Bound
+ *                                 (src/mpc.cpp:221-306)
+ *     OsqpEigen::Solver::{updateGradient, updateLinearConstraintsMatrix, updateBounds,
+ *                         initSolver, solve, getSolution}  (src/mpc.cpp:81-142,
+ *                         solver_ member at include/f110-mpc/mpc.h:63)
+ * f110qp_solve_batch[_dev] replaces that whole sequence for B ticks/candidates at once:
+ * linearisation, condensing, the QP solve and the (u*, x*) extraction of
+ * MPC::UpdateSolvedTrajectory (src/mpc.cpp:145-159) run in one HIP launch on gfx950.
+ *
+ * Conventions
+ *  - Plain C: no C++ exceptions cross this boundary; every entry point returns an int
+ *    (F110QP_OK = 0, negative = error; details from f110qp_last_error()).
+ *  - The caller owns every buffer. *_dev entry points take device pointers and a
+ *    hipStream_t (passed as void*) and are asynchronous on that stream; the host-pointer
+ *    entry points are synchronous.
+ *  - One f110qp_ctx per host thread. A ctx owns its device workspace.
+ *  - Layouts (row-major, float32):
+ *      x0        [B][3]      (x, y, ori)           State  (include/f110-mpc/state.h:10-45)
+ *      u_lin     [B][2]      (v, steer_ang)        Input  (include/f110-mpc/input.h:11-34)
+ *      x_ref     [B][N][3]   desired states 0..N-1 (the reference reads the first N of its
+ *                            50-point mini path; stage N reuses x_ref[N-1], mpc.cpp:228)
+ *      halfspace [B][2][3]   (l1, l2) = (a, b, c+0.5) from FindHalfSpaces, or NULL
+ *      u_out     [B][N][2]   u*_k = z[3(N+1)+2k .. +1]            (mpc.cpp:148-157)
+ *      x_out     [B][N+1][3] x*_k = z[3k .. 3k+2]                 (mpc.cpp:167-169)
+ *      status    [B]         F110QP_SOLVED / _PRIMAL_INFEASIBLE / _MAX_ITER (OSQP codes)
+ *      iters     [B]         active-set iterations (may be NULL)
+ *    On a non-SOLVED status u_out/x_out hold NaN, as OSQP's solution does on failure.
+ */
+#ifndef F110QP_H
+#define F110QP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define F110QP_API_VERSION 1
+
+/* return codes */
+#define F110QP_OK 0
+#define F110QP_ERR_INVALID -1     /* bad argument / unsupported configuration */
+#define F110QP_ERR_HIP -2         /* HIP runtime error (no device, launch failure, ...) */
+#define F110QP_ERR_ALLOC -3
+
+/* per-QP status codes (values follow OSQP's status ids) */
+#define F110QP_SOLVED 1
+#define F110QP_MAX_ITER -2
+#define F110QP_PRIMAL_INFEASIBLE -3
+#define F110QP_NUMERICAL -10      /* non-finite data or factorisation breakdown */
+
+/* gap (follow-the-gap half-space) row semantics, src/mpc.cpp:279-300 */
+#define F110QP_GAP_INACTIVE 0     /* as shipped: gap rows bounded by +-OsqpEigen::INFTY */
+#define F110QP_GAP_ACTIVE 1       /* a*x+b*y >= -(c+0.5) on stages 1..N (mpc.cpp:297-298) */
+
+#define F110QP_MAX_HORIZON 64
+
+typedef struct f110qp_ctx f110qp_ctx;
+
+typedef struct {
+  int horizon;      /* N; params.yaml:12 ("/horizon"), 1..F110QP_MAX_HORIZON          */
+  float dt;         /* params.yaml:13, held as float MPC::dt_ (include/f110-mpc/mpc.h:46) */
+  double q[3];      /* diag Q: q0,q1,q2 (params.yaml:1-3; mpc.cpp:20-24)                 */
+  double r[2];      /* diag R: r0,r1 (params.yaml:5-6)                                    */
+  double u_des[2];  /* des_vel, des_steer (params.yaml:42-43; mpc.cpp:18-19)              */
+  float u_min[2];   /* (umin, -0.43f) constraints.cpp:21                                  */
+  float u_max[2];   /* (umax,  0.43f) constraints.cpp:19                                  */
+  int gap_mode;     /* F110QP_GAP_INACTIVE | F110QP_GAP_ACTIVE                            */
+  int max_iter;     /* active-set iteration cap per QP (0 = default 8*(2N+2N))             */
+  int device;       /* HIP device ordinal used by the host-pointer entry points            */
+} f110qp_config;
+
+/* Library / ABI version (F110QP_API_VERSION). */
+int f110qp_version(void);
+/* Message of the last error on this thread (never NULL). */
+const char* f110qp_last_error(void);
+
+/* Defaults of params.yaml + constraints.cpp:19,21 for horizon N.
+ * Replaces the getParam block of MPC::MPC (src/mpc.cpp:5-24) and Constraints::Constraints
+ * (src/constraints.cpp:7-21). */
+void f110qp_default_config(f110qp_config* cfg, int horizon);
+
+/* Create a solver context (device workspace). Replaces the lazy OsqpEigen workspace set-up
+ * of MPC::Update's first call (src/mpc.cpp:96-131). */
+int f110qp_create(f110qp_ctx** ctx, const f110qp_config* cfg);
+void f110qp_destroy(f110qp_ctx* ctx);
+
+/* Solve B independent ticks (host pointers, synchronous). Replaces, per instance,
+ * MPC::Update's Linearize + gradient/constraint/bound updates + solver_.solve() +
+ * getSolution (src/mpc.cpp:69-143) and UpdateSolvedTrajectory (src/mpc.cpp:145-159). */
+int f110qp_solve_batch(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                       const float* x_ref, const float* halfspace, float* u_out, float* x_out,
+                       int* status, int* iters);
+
+/* Same on device pointers, enqueued on `stream` (a hipStream_t, NULL = default stream). */
+int f110qp_solve_batch_dev(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                           const float* x_ref, const float* halfspace, float* u_out,
+                           float* x_out, int* status, int* iters, void* stream);
+
+/* Debug/parity hook: the condensed Hessian H [B][2N][2N] and gradient g [B][2N] exactly as
+ * the solve kernel builds them on the device (float64), for comparison with the CPU oracle's
+ * condensing of the reference QP (src/mpc.cpp:208-306). Device pointers, async on stream. */
+int f110qp_condense_debug_dev(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                              const float* x_ref, double* H_out, double* g_out, void* stream);
+
+/* Constraints::FindHalfSpaces (src/constraints.cpp:116-265) for one scan, host code.
+ * state[3] = (x, y, ori); writes l1[3], l2[3] = (a, b, c+0.5). Returns F110QP_OK, or
+ * F110QP_ERR_INVALID when the scan holds no gap (the reference then reads ranges[-1]). */
+int f110qp_find_half_spaces(const double state[3], const float* ranges, int num_ranges,
+                            float angle_min, float angle_increment, float angle_max,
+                            float ftg_thresh, float divider, float buffer, double l1[3],
+                            double l2[3]);
+
+/* Batched FindHalfSpaces on the device: scans [B][num_ranges], states [B][3] -> hs [B][2][3]
+ * (float32, the f110qp_solve_batch halfspace layout); gap_lo/gap_hi [B] may be NULL. */
+int f110qp_find_half_spaces_dev(int batch, const float* states, const float* ranges,
+                                int num_ranges, float angle_min, float angle_increment,
+                                float angle_max, float ftg_thresh, float divider, float buffer,
+                                float* hs_out, int* gap_lo, int* gap_hi, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* F110QP_H */
