@@ -319,6 +319,17 @@ static int build_condensed(const f110o_params* prm, const double x0[3], const do
   return 0;
 }
 
+
+int f110o_condense(const f110o_params* prm, const double x0[3], const double ulin[2],
+                   const double* x_ref, double* H_out, double* g_out) {
+  condensed c;
+  build_condensed(prm, x0, ulin, x_ref, NULL, 0, &c);
+  const int nu = c.nu;
+  memcpy(H_out, c.H, (size_t)nu * nu * sizeof(double));
+  memcpy(g_out, c.g, (size_t)nu * sizeof(double));
+  condensed_free(&c);
+  return 0;
+}
 /* ------------------------------------------------------------------------------------------ */
 /* Goldfarb-Idnani dual active set, range-space form: maintains W = H^-1, the active normals'  */
 /* W n_j and a Cholesky factor of S_A = N_A' W N_A. Exact (finite) for strictly convex QPs.    */

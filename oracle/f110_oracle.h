@@ -74,6 +74,11 @@ int f110o_assemble(const f110o_params* prm, const double x0[3], const double u_l
                    int* P_rowind, double* P_val, double* q, int* A_colptr, int* A_rowind,
                    double* A_val, double* l, double* u);
 
+/* Condensed problem of one tick (dynamics rows eliminated): H [2N*2N] row-major, g [2N],
+ * objective 0.5 u'Hu + g'u (+ const), built from an explicit Gamma (float64). */
+int f110o_condense(const f110o_params* prm, const double x0[3], const double u_lin[2],
+                   const double* x_ref, double* H_out, double* g_out);
+
 /* Exact solve of the tick's QP (condensed, dual active-set, float64) and the OSQP-layout
  * primal z (n) and dual y (m) reconstructed on the full formulation.
  *   u_out[N*2], x_out[(N+1)*3] (may be NULL), z_out[n], y_out[m] (may be NULL).

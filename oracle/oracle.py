@@ -79,6 +79,7 @@ def lib():
                                              C.c_float, C.c_float, C.c_float, dp, dp, ip, ip]
         L.f110o_assemble.argtypes = [C.POINTER(Params), dp, dp, dp, dp, C.c_int, ip, ip, dp, dp,
                                      ip, ip, dp, dp, dp]
+        L.f110o_condense.argtypes = [C.POINTER(Params), dp, dp, dp, dp, dp]
         L.f110o_solve.argtypes = [C.POINTER(Params), dp, dp, dp, dp, C.c_int, dp, dp, dp, dp, dp, ip]
         L.f110o_kkt_residuals.argtypes = [C.POINTER(Params), dp, dp, dp, dp, C.c_int, dp, dp, dp]
         L.f110o_solve_batch.argtypes = [C.POINTER(Params), C.c_int, fp, fp, fp, fp, C.c_int, dp,
@@ -164,6 +165,15 @@ def assemble(prm: Params, x0, u_lin, x_ref, hs=None, gap_active=False):
                          _ptr(out["q"]), _ptr(out["A_colptr"], ip), _ptr(out["A_rowind"], ip), _ptr(out["A_val"]),
                          _ptr(out["l"]), _ptr(out["u"]))
     return out
+
+
+def condense(prm: Params, x0, u_lin, x_ref):
+    """Condensed (H, g) of one tick, float64, from an explicit Gamma."""
+    N = prm.horizon
+    H = np.zeros((2 * N, 2 * N))
+    g = np.zeros(2 * N)
+    lib().f110o_condense(C.byref(prm), _ptr(_d(x0)), _ptr(_d(u_lin)), _ptr(_d(x_ref).reshape(-1)), _ptr(H), _ptr(g))
+    return H, g
 
 
 def solve(prm: Params, x0, u_lin, x_ref, hs=None, gap_active=False):

@@ -1,0 +1,107 @@
+"""The C ABI library on the CPU: it loads, exports every symbol include/f110qp.h declares,
+mirrors the reference defaults and validates its arguments (no compute call needs a GPU)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+from conftest import ROOT
+
+
+def declared_symbols():
+    hdr = open(os.path.join(ROOT, "include", "f110qp.h")).read()
+    return sorted(set(re.findall(r"\b(f110qp_[a-z_]+)\s*\(", hdr)))
+
+
+def test_library_exports_every_declared_symbol(capi):
+    syms = declared_symbols()
+    assert len(syms) >= 10
+    assert set(syms) == set(capi.EXPORTED)
+    lib = C.CDLL(capi.LIB_PATH)
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_library_is_gfx950_code_object(capi):
+    data = open(capi.LIB_PATH, "rb").read()
+    assert b"gfx950" in data  # the offload bundle targets MI355X
+
+
+def test_version_and_defaults(capi):
+    L = capi.load()
+    assert L.f110qp_version() == 1
+    c = capi.default_config(20)
+    # params.yaml:1-13,42-47 and constraints.cpp:19,21
+    assert c.horizon == 20 and c.dt == np.float32(0.01)
+    assert list(c.q) == [10.0, 10.0, 0.0] and list(c.r) == [0.1, 5.0]
+    assert list(c.u_des) == [4.5, 0.0]
+    assert list(c.u_min) == [3.0, float(np.float32(-0.43))]
+    assert list(c.u_max) == [4.5, float(np.float32(0.43))]
+    assert c.gap_mode == capi.GAP_INACTIVE
+
+
+@pytest.mark.parametrize("over,msg", [
+    (dict(horizon=0), "horizon"),
+    (dict(horizon=33), "horizon"),
+    (dict(r=[0.0, 5.0]), "R must be > 0"),
+    (dict(q=[-1.0, 10.0, 0.0]), "Q must be"),
+    (dict(u_min=[5.0, -0.43]), "u_min > u_max"),
+    (dict(gap_mode=7), "gap_mode"),
+    (dict(dt=0.0), "dt"),
+    (dict(max_iter=-1), "max_iter"),
+])
+def test_create_rejects_bad_config(capi, over, msg):
+    c = capi.default_config(20)
+    for k, v in over.items():
+        if k in ("q", "r", "u_min", "u_max"):
+            for i, x in enumerate(v):
+                getattr(c, k)[i] = x
+        else:
+            setattr(c, k, v)
+    with pytest.raises(capi.F110QPError, match=msg):
+        capi.Solver(c)
+
+
+def test_solve_argument_validation_without_gpu(capi):
+    s = capi.Solver(capi.default_config(20))
+    L = capi.load()
+    # batch 0 is a no-op, negative batch / NULL buffers are rejected before any HIP call
+    assert L.f110qp_solve_batch_dev(s._h, 0, None, None, None, None, None, None, None, None, None) == capi.OK
+    assert L.f110qp_solve_batch_dev(s._h, -1, None, None, None, None, None, None, None, None, None) == capi.ERR_INVALID
+    assert L.f110qp_solve_batch_dev(s._h, 4, None, None, None, None, None, None, None, None, None) == capi.ERR_INVALID
+    assert "non-NULL" in capi.last_error()
+    assert L.f110qp_solve_batch_dev(None, 4, None, None, None, None, None, None, None, None, None) == capi.ERR_INVALID
+    g = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE))
+    buf = np.zeros(1024, np.float32)
+    p = C.c_void_p(buf.ctypes.data)
+    assert L.f110qp_solve_batch_dev(g._h, 4, p, p, p, None, p, p, p, None, None) == capi.ERR_INVALID
+    assert "halfspace" in capi.last_error()
+    s.close()
+    g.close()
+    capi.Solver(capi.default_config(20)).close()  # create/destroy never touches the device
+
+
+def test_find_half_spaces_no_gap_is_an_error(capi):
+    r = np.full(1080, 1.0, np.float32)
+    with pytest.raises(capi.F110QPError, match="no gap"):
+        capi.find_half_spaces([0, 0, 0], r, -np.pi, 2 * np.pi / 1080, np.pi)
+
+
+def test_product_does_not_import_the_oracle():
+    """The shipped path never routes through the checker (no CPU fallback)."""
+    pkg = os.path.join(ROOT, "f110-mpc_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h", ".hpp")) or f == "Makefile":
+                txt = open(os.path.join(dirpath, f), errors="ignore").read()
+                assert "import oracle" not in txt and "liboracle" not in txt and "f110_oracle" not in txt, f
+
+
+def test_capi_raises_when_library_missing(monkeypatch):
+    from f110qp import capi
+
+    monkeypatch.setattr(capi, "_lib", None)
+    monkeypatch.setattr(capi, "LIB_PATH", "/nonexistent/libf110qp.so")
+    with pytest.raises(capi.F110QPError, match="not built"):
+        capi.load()

@@ -1,0 +1,92 @@
+"""Sharding of a global batch over ranks, exercised with world_size 2 over
+gloo on the CPU: the gathered sharded result must be bit-identical to the one-process result."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from f110qp.shard import shard_range
+
+
+@pytest.mark.parametrize("total,world,align", [(65536, 8, 120), (1000, 3, 1), (7, 4, 1), (0, 2, 1), (240, 2, 120),
+                                               (65536, 1, 120), (121, 2, 120)])
+def test_shard_range_partitions(total, world, align):
+    owned = []
+    prev_hi = 0
+    for r in range(world):
+        lo, hi = shard_range(total, world, r, align)
+        assert lo == prev_hi and lo <= hi
+        if hi < total:
+            assert hi % align == 0
+        owned.append(hi - lo)
+        prev_hi = hi
+    assert prev_hi == total and sum(owned) == total
+    # balanced to within one group
+    assert max(owned) - min(owned) <= 2 * align  # one group plus the partial tail group
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "f110-mpc_amd"))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import torch.distributed as dist
+
+    import oracle
+    from f110qp import workload
+    from f110qp.shard import solve_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N = 20
+    w = workload.make_grouped_batch(3, N, seed=5, lanes=(0.0, 0.25), steers=5)  # 3 scenarios x 10
+    inputs = {k: torch.from_numpy(w[k]) for k in ("x0", "u_lin", "x_ref")}
+
+    def solve_fn(sh):
+        if sh["x0"].shape[0] == 0:
+            return {"u": torch.zeros((0, N, 2), dtype=torch.float64), "status": torch.zeros(0, dtype=torch.int32)}
+        u, x, st = oracle.solve_batch(oracle.params(N), sh["x0"].numpy(), sh["u_lin"].numpy(), sh["x_ref"].numpy())
+        return {"u": torch.from_numpy(u), "status": torch.from_numpy(st)}
+
+    out = solve_sharded(solve_fn, inputs, group_align=w["group_size"])
+    q.put((rank, out["u"].numpy(), out["status"].numpy()))
+    dist.destroy_process_group()
+
+
+def test_sharded_equals_single_process_gloo():
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "oracle"))
+    import oracle
+    from f110qp import workload
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    N = 20
+    w = workload.make_grouped_batch(3, N, seed=5, lanes=(0.0, 0.25), steers=5)
+    u, x, st = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"])
+    for rank, ug, sg in res:
+        np.testing.assert_array_equal(ug, u)
+        np.testing.assert_array_equal(sg, st)
