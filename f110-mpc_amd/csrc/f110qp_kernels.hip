@@ -29,6 +29,18 @@
 
 namespace f110qp {
 
+// Diagnostic build only (-DF110QP_STAMPS): per-phase s_memtime deltas of every wave, read back
+// with f110qp_read_stamps(). The shipped library never executes a stamp.
+#ifdef F110QP_STAMPS
+constexpr int kStampSlots = 8;
+__device__ unsigned long long g_stamps[65536 * kStampSlots];
+#define STAMP(var) unsigned long long var = __builtin_amdgcn_s_memtime()
+#define STAMP_ACC(acc, since) acc += __builtin_amdgcn_s_memtime() - (since)
+#else
+#define STAMP(var)
+#define STAMP_ACC(acc, since)
+#endif
+
 // ------------------------------------------------------------------------------------------
 // wave helpers (64 lanes)
 // ------------------------------------------------------------------------------------------
@@ -311,6 +323,10 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
   const int a = lane & 1;    // 0 = speed v, 1 = steering
   const bool valid = lane < NU;
 
+  STAMP(t_start);
+#ifdef F110QP_STAMPS
+  unsigned long long acc_refine = 0;
+#endif
   // ---- 1. inputs + Model::Linearize ----------------------------------------------------
   const float fX0 = x0g[3 * b + 0], fY0 = x0g[3 * b + 1], fTH0 = x0g[3 * b + 2];
   const double X0 = (double)fX0, Y0 = (double)fY0;
@@ -349,6 +365,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
   }
   wsync();
 
+  STAMP(t_lin);
   // ---- 2a. gradient at u = 0 (fp64 adjoint) and the free response ------------------------
   float cgap = 0.f, gnorm = 1.f;
   {
@@ -367,6 +384,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
     }
   }
 
+  STAMP(t_grad);
   // ---- 2b. condensed Hessian row (closed form, fp32) --------------------------------------
   float hrow[NUM];
   {
@@ -410,6 +428,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
   const float g32 = sm.vec[lane];
   wsync();
 
+  STAMP(t_hess);
   // ---- 3. W = H^-1 : symmetric sweep (Goodnight), row `lane` in registers ----------------
   Sweep<NUM, 0>::run(sm, hrow, lane);
   if (lane < NUM) {
@@ -418,6 +437,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
   }
   wsync();
 
+  STAMP(t_inv);
   // ---- 4. dual active set (Goldfarb-Idnani, range space) ---------------------------------
   // x = -W g
   sm.vec[lane] = g32;
@@ -474,6 +494,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
         sp = __shfl(sraw, bid / 3, 64);
       } else {
         // ---- 5. refinement in fp64 + exact feasibility re-check ----
+        STAMP(t_ref0);
         sm.cmult[3 * lane] = 0.f;
         sm.cmult[3 * lane + 1] = 0.f;
         sm.cmult[3 * lane + 2] = 0.f;
@@ -552,6 +573,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
           }
         }
         wave_argmin(best64, bid64);
+        STAMP_ACC(acc_refine, t_ref0);
         if (bid64 == 0x7fffffff || reentries >= 4) {
           final_ok = true;
           break;
@@ -689,6 +711,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
     }
   }
 
+  STAMP(t_gi);
   // ---- 6. outputs ---------------------------------------------------------------------------
   if (status == F110QP_SOLVED_ID && !final_ok) status = F110QP_MAX_ITER_ID;
   const bool ok = (status == F110QP_SOLVED_ID);
@@ -711,6 +734,14 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
     status_out[b] = status;
     if (iters_out) iters_out[b] = it;
   }
+#ifdef F110QP_STAMPS
+  STAMP(t_end);
+  if (lane == 0 && b < 65536) {
+    unsigned long long* o = g_stamps + (size_t)b * kStampSlots;
+    o[0] = t_lin - t_start; o[1] = t_grad - t_lin; o[2] = t_hess - t_grad; o[3] = t_inv - t_hess;
+    o[4] = t_gi - t_inv - acc_refine; o[5] = acc_refine; o[6] = t_end - t_gi; o[7] = t_end - t_start;
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -757,3 +788,10 @@ hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const
 }
 
 }  // namespace f110qp
+
+#ifdef F110QP_STAMPS
+extern "C" int f110qp_read_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(f110qp::g_stamps),
+                                  (size_t)n * f110qp::kStampSlots * sizeof(unsigned long long));
+}
+#endif

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libf110qp.so")
+# F110QP_LIB selects a diagnostic build (e.g. lib_stamps/); default is the in-tree library
+LIB_PATH = os.environ.get("F110QP_LIB", os.path.join(PKG_ROOT, "lib", "libf110qp.so"))
 
 OK = 0
 ERR_INVALID = -1
