@@ -32,7 +32,7 @@ namespace f110qp {
 // Diagnostic build only (-DF110QP_STAMPS): per-phase s_memtime deltas of every wave, read back
 // with f110qp_read_stamps(). The shipped library never executes a stamp.
 #ifdef F110QP_STAMPS
-constexpr int kStampSlots = 8;
+constexpr int kStampSlots = 16;
 __device__ unsigned long long g_stamps[65536 * kStampSlots];
 #define STAMP(var) unsigned long long var = __builtin_amdgcn_s_memtime()
 #define STAMP_ACC(acc, since) acc += __builtin_amdgcn_s_memtime() - (since)
@@ -42,45 +42,51 @@ __device__ unsigned long long g_stamps[65536 * kStampSlots];
 #endif
 
 // ------------------------------------------------------------------------------------------
-// wave helpers (64 lanes)
+// wave helpers (64 lanes). Cross-lane traffic uses DPP (row shifts / quad permutes /
+// row broadcasts) and readlane, never LDS: every helper is a handful of VALU instructions.
+// They must be called from wave-uniform control flow (all 64 lanes active): readlane of an
+// EXEC-disabled lane returns a stale register, and DPP treats disabled sources as invalid.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+// DPP controls (gfx9 family encodings)
+constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118;
+constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143;
+constexpr int DPP_QUAD_XOR1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;  // quad_perm [2,3,0,1]
+constexpr int DPP_QUAD_ODD = 0xF5;   // quad_perm [1,1,3,3]: every lane gets lane|1
+constexpr int DPP_ROW_HALF_MIRROR = 0x141, DPP_ROW_MIRROR = 0x140;
 
-// argmin of (val, idx); ties -> smaller idx
-__device__ __forceinline__ void wave_argmin(float& val, int& idx) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    float ov = __shfl_xor(val, o, 64);
-    int oi = __shfl_xor(idx, o, 64);
-    if (ov < val || (ov == val && oi < idx)) { val = ov; idx = oi; }
-  }
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ int dpp_i(int v) {  // lanes without a source read 0
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xf, false);
 }
-
-template <typename T>
-__device__ __forceinline__ T scan_incl(T x, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    T t = __shfl_up(x, o, 64);
-    if (lane >= o) x += t;
-  }
-  return x;
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(dpp_i<CTRL, ROWMASK>(__float_as_int(v)));
 }
-
-template <typename T>
-__device__ __forceinline__ T scan_suffix_incl(T x, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    T t = __shfl_down(x, o, 64);
-    if (lane + o < 64) x += t;
-  }
-  return x;
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v) {
+  int2 p = *reinterpret_cast<int2*>(&v);
+  p.x = dpp_i<CTRL, ROWMASK>(p.x);
+  p.y = dpp_i<CTRL, ROWMASK>(p.y);
+  return *reinterpret_cast<double*>(&p);
+}
+// full-permutation DPPs (every lane has a source)
+template <int CTRL>
+__device__ __forceinline__ float perm_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int perm_i(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double perm_d(double v) {
+  int2 p = *reinterpret_cast<int2*>(&v);
+  p.x = __builtin_amdgcn_mov_dpp(p.x, CTRL, 0xf, 0xf, false);
+  p.y = __builtin_amdgcn_mov_dpp(p.y, CTRL, 0xf, 0xf, false);
+  return *reinterpret_cast<double*>(&p);
 }
 
 __device__ __forceinline__ float readlane_f(float v, int l) {
@@ -92,6 +98,66 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   p.x = __builtin_amdgcn_readlane(p.x, l);
   p.y = __builtin_amdgcn_readlane(p.y, l);
   return *reinterpret_cast<double*>(&p);
+}
+
+// inclusive prefix sum over the 64 lanes (row shifts, then row broadcasts 15 and 31)
+__device__ __forceinline__ float scan_incl(float x, int) {
+  x += dpp_f<DPP_ROW_SHR1>(x);
+  x += dpp_f<DPP_ROW_SHR2>(x);
+  x += dpp_f<DPP_ROW_SHR4>(x);
+  x += dpp_f<DPP_ROW_SHR8>(x);
+  x += dpp_f<DPP_ROW_BCAST15, 0xa>(x);
+  x += dpp_f<DPP_ROW_BCAST31, 0xc>(x);
+  return x;
+}
+__device__ __forceinline__ double scan_incl(double x, int) {
+  x += dpp_d<DPP_ROW_SHR1>(x);
+  x += dpp_d<DPP_ROW_SHR2>(x);
+  x += dpp_d<DPP_ROW_SHR4>(x);
+  x += dpp_d<DPP_ROW_SHR8>(x);
+  x += dpp_d<DPP_ROW_BCAST15, 0xa>(x);
+  x += dpp_d<DPP_ROW_BCAST31, 0xc>(x);
+  return x;
+}
+// inclusive suffix sum: total - inclusive prefix + own
+template <typename T>
+__device__ __forceinline__ T scan_suffix_incl(T x, int lane) {
+  const T p = scan_incl(x, lane);
+  T tot;
+  if constexpr (sizeof(T) == 8) tot = readlane_d(p, 63);
+  else tot = readlane_f(p, 63);
+  return tot - p + x;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+  const T p = scan_incl(v, 0);
+  if constexpr (sizeof(T) == 8) return readlane_d(p, 63);
+  else return readlane_f(p, 63);
+}
+
+// value of lane|1 (the steering lane of the stage pair)
+__device__ __forceinline__ float odd_lane(float v) { return perm_f<DPP_QUAD_ODD>(v); }
+__device__ __forceinline__ double odd_lane(double v) { return perm_d<DPP_QUAD_ODD>(v); }
+
+// argmin of (val, idx) over the wave, result uniform; ties -> smaller idx
+__device__ __forceinline__ void amin_step(float& v, int& i, float ov, int oi) {
+  const bool take = (ov < v) || (ov == v && oi < i);
+  v = take ? ov : v;
+  i = take ? oi : i;
+}
+__device__ __forceinline__ void wave_argmin(float& val, int& idx) {
+  amin_step(val, idx, perm_f<DPP_QUAD_XOR1>(val), perm_i<DPP_QUAD_XOR1>(idx));
+  amin_step(val, idx, perm_f<DPP_QUAD_XOR2>(val), perm_i<DPP_QUAD_XOR2>(idx));
+  amin_step(val, idx, perm_f<DPP_ROW_HALF_MIRROR>(val), perm_i<DPP_ROW_HALF_MIRROR>(idx));
+  amin_step(val, idx, perm_f<DPP_ROW_MIRROR>(val), perm_i<DPP_ROW_MIRROR>(idx));
+  float v0 = readlane_f(val, 0);
+  int i0 = readlane_i(idx, 0);
+  amin_step(v0, i0, readlane_f(val, 16), readlane_i(idx, 16));
+  amin_step(v0, i0, readlane_f(val, 32), readlane_i(idx, 32));
+  amin_step(v0, i0, readlane_f(val, 48), readlane_i(idx, 48));
+  val = v0;
+  idx = i0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -132,8 +198,7 @@ __device__ __forceinline__ void rollout_f64(const Lin& M, int lane, double uval,
   s1 = scan_incl(s1, lane);
   s2 = scan_incl(s2, lane);
   s3 = scan_incl(s3, lane);
-  const int src = lane | 1;
-  const double P1 = __shfl(s1, src, 64), P2 = __shfl(s2, src, 64), V = __shfl(s3, src, 64);
+  const double P1 = odd_lane(s1), P2 = odd_lane(s2), V = odd_lane(s3);
   const double i = (double)(k + 1);
   th = M.th0 + i * M.c2 + P1;
   const double sth = i * M.th0 + M.c2 * (i * (i - 1.0) * 0.5) + (i - 1.0) * P1 - P2;
@@ -153,8 +218,7 @@ __device__ __forceinline__ void rollout_lin_f32(float a02, float a12, float b00,
   s1 = scan_incl(s1, lane);
   s2 = scan_incl(s2, lane);
   s3 = scan_incl(s3, lane);
-  const int src = lane | 1;
-  const float P1 = __shfl(s1, src, 64), P2 = __shfl(s2, src, 64), V = __shfl(s3, src, 64);
+  const float P1 = odd_lane(s1), P2 = odd_lane(s2), V = odd_lane(s3);
   const float sth = (float)k * P1 - P2;  // (i-1)P1 - P2 with i = k+1
   X = a02 * sth + b00 * V;
   Y = a12 * sth + b10 * V;
@@ -199,24 +263,25 @@ struct Smem {
   float stX[33], stY[33];  // per-stage linear rollout (stage 1..N)
   float rx[64], ry[64], rth[64];  // recentred reference of the lane's stage
   float cmult[3 * 64];     // multiplier per constraint id
+  int ids[64];             // PDAS: constraint id of each active slot
+  float pmu[64];           // PDAS: multiplier of each variable's active bound
   double d64[64];
   double sx64[33], sy64[33];
   Lin M;                   // linearisation of this QP (uniform)
 };
 
 // l = L^-1 v, one lane per active slot (v, l in lane j for slot j < q); L read from LDS.
+// A plain q-step loop: the slot count is uniform, each step is mul -> readlane -> fma.
 template <int NUM>
 __device__ __forceinline__ float tri_forward(Smem<NUM>& sm, int lane, int q, float rdiag,
                                              float v) {
   float acc = v, lv = 0.f;
-#pragma unroll
-  for (int kk = 0; kk < NUM; kk++) {
-    if (kk >= q) break;
+  const int row = lane < NUM ? lane : NUM - 1;
+  for (int kk = 0; kk < q; kk++) {
     const float t = acc * rdiag;
     const float lk = readlane_f(t, kk);
-    if (lane == kk) lv = t;
-    const float Ljk = (lane < q) ? sm.L[lane][kk] : 0.f;
-    acc = fmaf(-Ljk, lk, acc);
+    lv = (lane == kk) ? t : lv;
+    acc = fmaf(-sm.L[row][kk], lk, acc);
   }
   return lv;
 }
@@ -226,16 +291,32 @@ template <int NUM>
 __device__ __forceinline__ float tri_backward(Smem<NUM>& sm, int lane, int q, float rdiag,
                                               float l) {
   float acc = l, r = 0.f;
-#pragma unroll
-  for (int jj = NUM - 1; jj >= 0; jj--) {
-    if (jj >= q) continue;
+  const int col = lane < NUM ? lane : NUM - 1;
+  for (int jj = q - 1; jj >= 0; jj--) {
     const float t = acc * rdiag;
     const float rj = readlane_f(t, jj);
-    if (lane == jj) r = t;
-    const float Ljl = (lane < q) ? sm.L[jj][lane] : 0.f;
-    acc = fmaf(-Ljl, rj, acc);
+    r = (lane == jj) ? t : r;
+    acc = fmaf(-sm.L[jj][col], rj, acc);
   }
   return r;
+}
+
+// L = chol(S_A) of the q active slots (left-looking, one lane per row, S and L in LDS).
+// Returns this lane's 1/L[lane][lane] (unchanged value `rd` for lanes >= q).
+template <int NUM>
+__device__ __forceinline__ float chol_slots(Smem<NUM>& sm, int lane, int q, float rd) {
+  for (int c = 0; c < q; c++) {
+    float s = 0.f;
+    if (lane < q && lane >= c) {
+      s = sm.S[lane][c];
+      for (int i2 = 0; i2 < c; i2++) s = fmaf(-sm.L[lane][i2], sm.L[c][i2], s);
+    }
+    const float dcc = sqrtf(readlane_f(s, c));
+    if (lane < q && lane >= c) sm.L[lane][c] = (lane == c) ? dcc : s / dcc;
+    if (lane == c) rd = 1.f / dcc;
+    wsync();
+  }
+  return rd;
 }
 
 // y_lane = sum_j W[lane][j] x_j with x in sm.vec; W symmetric so lane reads column `lane`
@@ -263,20 +344,15 @@ __device__ __forceinline__ float slot_dot(Smem<NUM>& sm, int slot_id, float ga0,
 
 // One pivot of the symmetric sweep operator (Goodnight 1979) on the row held by this lane:
 //   a_ij -= a_ip a_pj / a_pp ; a_ip /= a_pp ; a_pj /= a_pp ; a_pp = -1/a_pp.
-// The pivot row is broadcast through LDS; its own update folds into the common FMA with
+// The pivot row is broadcast with readlane; its own update folds into the common FMA with
 // f = 1 - 1/a_pp. After all pivots the rows hold -H^-1. P is a template constant so every
 // register index is static (no scratch).
 template <int NUM, int P>
-__device__ __forceinline__ void sweep_step(Smem<NUM>& sm, float (&hrow)[NUM], int lane) {
-  if (lane == P) {
-#pragma unroll
-    for (int j = 0; j < NUM; j++) sm.W[0][j] = hrow[j];
-  }
-  wsync();
+__device__ __forceinline__ void sweep_step(Smem<NUM>&, float (&hrow)[NUM], int lane) {
+  // pivot row broadcast by readlane (lane P, static register index) -> SGPR operands
   float rk[NUM];
 #pragma unroll
-  for (int j = 0; j < NUM; j++) rk[j] = sm.W[0][j];
-  wsync();
+  for (int j = 0; j < NUM; j++) rk[j] = readlane_f(hrow[j], P);
   const float inv = 1.f / rk[P];
   const bool piv = (lane == P);
   const float f = piv ? (1.f - inv) : hrow[P] * inv;
@@ -325,7 +401,8 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
 
   STAMP(t_start);
 #ifdef F110QP_STAMPS
-  unsigned long long acc_refine = 0;
+  unsigned long long acc_refine = 0, acc_s1 = 0, acc_w = 0, acc_vj = 0, acc_tri = 0, acc_z = 0,
+                     acc_step = 0, acc_upd = 0, acc_pdas = 0;
 #endif
   // ---- 1. inputs + Model::Linearize ----------------------------------------------------
   const float fX0 = x0g[3 * b + 0], fY0 = x0g[3 * b + 1], fTH0 = x0g[3 * b + 2];
@@ -372,9 +449,10 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
     const Lin M = sm.M;
     double px0, py0, th0s;
     rollout_f64(M, lane, 0.0, px0, py0, th0s);
-    const double g64 = valid ? grad_f64(M, P, lane, N, 0.0, px0, py0, th0s, (double)sm.rx[lane],
-                                        (double)sm.ry[lane], (double)sm.rth[lane], 0.0, 0.0)
-                             : 0.0;
+    // cross-lane helpers run with all 64 lanes active (lanes >= 2N contribute zeros)
+    const double g64a = grad_f64(M, P, lane, N, 0.0, px0, py0, th0s, (double)sm.rx[lane],
+                                 (double)sm.ry[lane], (double)sm.rth[lane], 0.0, 0.0);
+    const double g64 = valid ? g64a : 0.0;
     sm.vec[lane] = (float)g64;
     if (Hdbg && valid) gdbg[(size_t)b * NU + lane] = g64;
     if (GAP) {
@@ -459,8 +537,85 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
   int forced_p = -1;     // violated row found by the fp64 re-check
   float forced_sp = 0.f;
 
+  // ---- 4a. box rows only: primal-dual active set warm start (Hintermueller-Ito-Kunisch) ----
+  // Each pass solves the equality QP of the current guess by one Schur solve with S_A =
+  // W[A][A] and re-guesses A from the multipliers and the bounds; on these QPs it reaches
+  // the optimal set in <= 5 passes (one-at-a-time GI needs one pass per active bound). Its
+  // fixed point is a valid GI state (independent normals, positive multipliers), so the GI
+  // loop below only confirms it, and resumes from it if the fp64 re-check finds a violated
+  // row. No convergence within kPdasMaxIter passes -> plain GI from the unconstrained point.
+  if (!GAP && status == F110QP_SOLVED_ID) {
+    STAMP(t_pdas);
+    constexpr int kPdasMaxIter = 10;
+    const float uunc = xv;
+    sm.vec[lane] = uunc;
+    int act = 0;  // 0 free, 1 at the lower bound, 2 at the upper bound
+    for (int pit = 0; pit < kPdasMaxIter; pit++) {
+      const unsigned long long mask = __ballot(act != 0);
+      const int qn = __popcll(mask);
+      const int myslot = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
+      if (act) sm.ids[myslot] = 3 * lane + (act == 2 ? 1 : 0);
+      wsync();
+      const int sid = (lane < qn) ? sm.ids[lane] : 0;
+      const int svar = sid / 3;
+      const float ssg = (sid - 3 * svar == 0) ? 1.f : -1.f;
+      float rhs = 0.f;
+      if (lane < qn) {
+        const float bj = (ssg > 0.f) ? ((svar & 1) ? umin1 : umin0) : -((svar & 1) ? umax1 : umax0);
+        rhs = bj - ssg * sm.vec[svar];  // b_j - n_j' u_unc
+        for (int l = 0; l < qn; l++) {
+          const int idl = sm.ids[l];
+          const int vl = idl / 3;
+          const float sgl = (idl - 3 * vl == 0) ? 1.f : -1.f;
+          sm.S[lane][l] = ssg * sgl * sm.W[svar][vl];
+        }
+      }
+      wsync();
+      const float rdp = chol_slots<NUM>(sm, lane, qn, 0.f);
+      const float lvp = tri_forward<NUM>(sm, lane, qn, rdp, rhs);
+      const float mu = tri_backward<NUM>(sm, lane, qn, rdp, lvp);
+      // u = u_unc + sum_j mu_j W n_j
+      float u = uunc;
+      const int cl = lane < NUM ? lane : NUM - 1;
+      for (int j = 0; j < qn; j++) {
+        const int vj = readlane_i(svar, j);
+        u = fmaf(readlane_f(mu * ssg, j), sm.W[vj][cl], u);
+      }
+      if (lane < qn) sm.pmu[svar] = mu;
+      wsync();
+      const float myu = act ? sm.pmu[lane] : 0.f;
+      const bool nlo = valid && ((act == 1 ? myu : 0.f) + (lb - u) > 0.f);
+      const bool nhi = valid && !nlo && ((act == 2 ? myu : 0.f) + (u - ub) > 0.f);
+      const int nact = nlo ? 1 : (nhi ? 2 : 0);
+      const bool changed = __ballot(nact != act) != 0;
+      wsync();
+      if (!changed) {
+        // converged: hand the active set to the GI state
+        q = qn;
+        slot_id = (lane < qn) ? sid : -1;
+        mult = (lane < qn) ? fmaxf(mu, 0.f) : 0.f;
+        rdiag = (lane < qn) ? rdp : 0.f;
+        actf = act;  // bit0 lower, bit1 upper
+        if (lane < NUM)
+          for (int j = 0; j < qn; j++) {
+            const int idj = sm.ids[j];
+            const int vj = idj / 3;
+            sm.V[j][lane] = ((idj - 3 * vj == 0) ? 1.f : -1.f) * sm.W[vj][lane];
+          }
+        xv = valid ? u : 0.f;
+        it = pit + 1;
+        wsync();
+        break;
+      }
+      act = nact;
+    }
+    STAMP_ACC(acc_pdas, t_pdas);
+  }
+
   while (status == F110QP_SOLVED_ID && !final_ok) {
     // ---- step 1: most violated inactive constraint (fp32, scaled) ----
+    STAMP(t_s1);
     int p;
     float sp;
     if (forced_p >= 0) {
@@ -491,7 +646,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
       wave_argmin(best, bid);
       if (bid != 0x7fffffff) {
         p = bid;
-        sp = __shfl(sraw, bid / 3, 64);
+        sp = readlane_f(sraw, bid / 3);
       } else {
         // ---- 5. refinement in fp64 + exact feasibility re-check ----
         STAMP(t_ref0);
@@ -514,7 +669,8 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
             gmx = m0 * ga0 + m1 * ga1;
             gmy = m0 * gb0 + m1 * gb1;
           }
-          double r1 = valid ? grad_f64(M, P, lane, N, u64, px, py, th, rxd, ryd, rthd, gmx, gmy) : 0.0;
+          const double r1a = grad_f64(M, P, lane, N, u64, px, py, th, rxd, ryd, rthd, gmx, gmy);
+          double r1 = valid ? r1a : 0.0;
           if (valid) r1 += -(double)sm.cmult[3 * lane] + (double)sm.cmult[3 * lane + 1];
           sm.d64[lane] = u64;
           if (GAP && a == 1 && k < N) { sm.sx64[k + 1] = px; sm.sy64[k + 1] = py; }
@@ -580,16 +736,18 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
         }
         reentries++;
         forced_p = bid64;
-        forced_sp = __shfl(sp64, bid64 / 3, 64);
+        forced_sp = readlane_f(sp64, bid64 / 3);
         xv = valid ? (float)u64 : 0.f;
         continue;
       }
     }
 
+    STAMP_ACC(acc_s1, t_s1);
     const int pown = p / 3, pt = p - 3 * pown;
     float uplus_new = 0.f;  // multiplier of the candidate p
     // ---- step 2: add p (possibly after drops) ----
     for (;;) {
+      STAMP(t_a);
       if (++it > max_iter) { status = F110QP_MAX_ITER_ID; break; }
       // w = W n_p ; nw = n_p' W n_p
       float w, nw;
@@ -613,6 +771,8 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
         w = matvec_W<NUM>(sm, lane);
         nw = wave_sum(np * w);
       }
+      STAMP_ACC(acc_w, t_a);
+      STAMP(t_b);
       // v_j = n_j' w for the active slots
       sm.vec2[lane] = w;
       if (GAP) {
@@ -624,15 +784,21 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
       }
       wsync();
       const float vj = (lane < q) ? slot_dot<NUM>(sm, slot_id, ga0, ga1, gb0, gb1) : 0.f;
+      STAMP_ACC(acc_vj, t_b);
+      STAMP(t_c);
       // l = L^-1 v ; r = L^-T l  (r = S_A^-1 N_A' W n_p : dual step direction)
       const float lv = tri_forward<NUM>(sm, lane, q, rdiag, vj);
       const float ll = wave_sum(lane < q ? lv * lv : 0.f);
       const float r = tri_backward<NUM>(sm, lane, q, rdiag, lv);
+      STAMP_ACC(acc_tri, t_c);
+      STAMP(t_d);
       // z = w - sum_j r_j V[j]  (primal step direction)
       float z = w;
       const int cl = lane < NUM ? lane : NUM - 1;
       for (int j = 0; j < q; j++) z = fmaf(-readlane_f(r, j), sm.V[j][cl], z);
       const float pivv = nw - ll;  // = z' n_p, the new Schur pivot
+      STAMP_ACC(acc_z, t_d);
+      STAMP(t_e);
       // partial step t1 (blocking multiplier k1)
       float t1 = 3.0e38f;
       int k1 = 0x7fffffff;
@@ -651,6 +817,8 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
         add = (t2 <= t1);
       }
       wsync();
+      STAMP_ACC(acc_step, t_e);
+      STAMP(t_f);
       if (add) {
         if (q >= NUM) { status = F110QP_MAX_ITER_ID; break; }
         if (lane < NUM) sm.V[q][lane] = w;
@@ -671,6 +839,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
         if (lane == pown) actf |= (1 << pt);
         q++;
         wsync();
+        STAMP_ACC(acc_upd, t_f);
         break;
       }
       // drop slot k1, then retry p
@@ -695,18 +864,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
           for (int i2 = kd; i2 < q - 1; i2++) sm.S[lane][i2] = sm.S[lane][i2 + 1];
         q--;
         wsync();
-        // refactor L = chol(S_A) (left-looking, one lane per row)
-        for (int c = 0; c < q; c++) {
-          float s = 0.f;
-          if (lane < q && lane >= c) {
-            s = sm.S[lane][c];
-            for (int i2 = 0; i2 < c; i2++) s = fmaf(-sm.L[lane][i2], sm.L[c][i2], s);
-          }
-          const float dcc = sqrtf(readlane_f(s, c));
-          if (lane < q && lane >= c) sm.L[lane][c] = (lane == c) ? dcc : s / dcc;
-          if (lane == c) rdiag = 1.f / dcc;
-          wsync();
-        }
+        rdiag = chol_slots<NUM>(sm, lane, q, rdiag);
       }
     }
   }
@@ -740,6 +898,9 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
     unsigned long long* o = g_stamps + (size_t)b * kStampSlots;
     o[0] = t_lin - t_start; o[1] = t_grad - t_lin; o[2] = t_hess - t_grad; o[3] = t_inv - t_hess;
     o[4] = t_gi - t_inv - acc_refine; o[5] = acc_refine; o[6] = t_end - t_gi; o[7] = t_end - t_start;
+    o[8] = acc_s1; o[9] = acc_w; o[10] = acc_vj; o[11] = acc_tri; o[12] = acc_z; o[13] = acc_step;
+    o[14] = acc_upd; o[15] = it; o[8] += 0; o[13] += 0; o[12] += 0; (void)acc_pdas;
+    o[9] = acc_pdas;
   }
 #endif
 }

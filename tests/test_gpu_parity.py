@@ -101,7 +101,10 @@ def test_true_heading_and_hard_references(oracle, capi):
     many active rows (both box faces)."""
     w = workload.make_batch(1024, 20, seed=77, heading="true", lateral=2.0, steer_range=1.2)
     u, x, st, it = check(oracle, capi, 20, w)
-    assert it.max() >= 10
+    lo = np.float32([3.0, -0.43])
+    hi = np.float32([4.5, 0.43])
+    n_active = ((np.abs(u - lo) < 1e-6) | (np.abs(u - hi) < 1e-6)).sum(axis=(1, 2))
+    assert n_active.max() >= 10 and ((np.abs(u[..., 1] - lo[1]) < 1e-6).any() and (np.abs(u[..., 1] - hi[1]) < 1e-6).any())
 
 
 def test_custom_weights(oracle, capi):

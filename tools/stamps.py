@@ -24,13 +24,18 @@ if gap:
 s = capi.Solver(capi.default_config(N, gap_mode=1 if gap else 0))
 for _ in range(3):
     u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
-buf = np.zeros((B, 8), np.uint64)
+buf = np.zeros((B, 16), np.uint64)
 L.f110qp_read_stamps.argtypes = [C.c_void_p, C.c_int]
 L.f110qp_read_stamps(C.c_void_p(buf.ctypes.data), B)
 names = ["inputs+linearize", "gradient g (fp64 scans)", "hessian (closed form)", "sweep inverse", "active set (fp32)",
-         "refinement+fp64 check", "outputs", "total"]
+         "refinement+fp64 check", "outputs", "total", " gi: step1 search", " pdas warm start (box)", " gi: v_j gather",
+         " gi: tri solves", " gi: z update", " gi: step lengths", " gi: append slot"]
 tot = buf[:, 7].astype(float)
 print(f"B={B} N={N} gap={gap} iters mean {it.mean():.2f} max {it.max()}")
 for i, n in enumerate(names):
+    if i >= 8 and buf[:, 15].sum() == 0:
+        break
     v = buf[:, i].astype(float)
     print(f"{n:28s} mean {v.mean():9.0f}  max {v.max():9.0f}  share {v.mean() / tot.mean() * 100:5.1f}%")
+it_ = buf[:, 15].astype(float)
+print(f"per-iteration: gi cycles/iter {(buf[:, 4].astype(float).sum() / max(1, it_.sum())):.0f}")
