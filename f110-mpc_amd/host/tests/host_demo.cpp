@@ -1,0 +1,117 @@
+// host_demo — drives the ROS-free C++ class surface (MPC / Constraints / Model / Cost / State /
+// Input / LoadParams) for the pytest suite.
+//   host_demo cpu <params.yaml>                         host-only checks, JSON on stdout
+//   host_demo tick <params.yaml> <in.bin> <out.bin>     MPC::Update over T ticks (GPU)
+//   host_demo batch <params.yaml> <in.bin> <out.bin>    MPC::UpdateBatch over B candidates (GPU)
+// in.bin (float32): T, N, then per tick x0[3], u_lin[2], x_ref[N*3]; gap mode adds
+// scan geometry (3) + R ranges per tick after an R header.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "f110mpc/mpc.h"
+
+static std::vector<float> read_all(const char* path) {
+  std::ifstream f(path, std::ios::binary);
+  f.seekg(0, std::ios::end);
+  const size_t n = static_cast<size_t>(f.tellg()) / 4;
+  f.seekg(0);
+  std::vector<float> v(n);
+  f.read(reinterpret_cast<char*>(v.data()), n * 4);
+  return v;
+}
+
+static int cpu(const char* params_path) {
+  Params p;
+  if (!LoadParams(params_path, &p)) return 2;
+  std::printf("{\"params\": {\"q\": [%.17g, %.17g, %.17g], \"r\": [%.17g, %.17g], \"horizon\": %d, "
+              "\"dt\": %.17g, \"des_vel\": %.17g, \"umax\": %.17g, \"umin\": %.17g, \"buffer\": %.17g, "
+              "\"fov_divider\": %.9g, \"follow_gap_thresh\": %.9g},\n",
+              p.q0, p.q1, p.q2, p.r0, p.r1, p.horizon, (double)p.dt, p.des_vel, (double)p.umax, (double)p.umin, (double)p.buffer,
+              (double)p.fov_divider, (double)p.follow_gap_thresh);
+  Model m;
+  State s(1.0, 2.0, 0.5);
+  Input in(4.5, 0.2);
+  m.Linearize(s, in, p.dt);
+  const auto A = m.A();
+  const auto B = m.B();
+  const auto C = m.C();
+  std::printf("\"linearize\": {\"A02\": %.17g, \"A12\": %.17g, \"B00\": %.17g, \"B10\": %.17g, "
+              "\"B20\": %.17g, \"B21\": %.17g, \"C\": [%.17g, %.17g, %.17g]},\n",
+              A[0][2], A[1][2], B[0][0], B[1][0], B[2][0], B[2][1], C[0], C[1], C[2]);
+  State ns;
+  m.simulate_dynamics(s, in, 0.01, ns);
+  std::printf("\"simulate\": [%.17g, %.17g, %.17g],\n", ns.x(), ns.y(), ns.ori());
+  Constraints c(p);
+  std::printf("\"u_min\": [%.17g, %.17g], \"u_max\": [%.17g, %.17g],\n", c.u_min()[0], c.u_min()[1],
+              c.u_max()[0], c.u_max()[1]);
+  LaserScan scan;
+  scan.angle_min = static_cast<float>(-M_PI);
+  scan.angle_increment = static_cast<float>(2 * M_PI / 1080);
+  scan.angle_max = scan.angle_min + scan.angle_increment * 1079;
+  scan.ranges.assign(1080, 1.5f);
+  for (int i = 480; i < 560; i++) scan.ranges[i] = 6.0f;
+  State car(3.0, -4.0, 0.3);
+  const bool ok = c.FindHalfSpaces(car, scan);
+  std::printf("\"half_spaces\": {\"ok\": %s, \"l1\": [%.17g, %.17g, %.17g], \"l2\": [%.17g, %.17g, %.17g]},\n",
+              ok ? "true" : "false", c.l1()[0], c.l1()[1], c.l1()[2], c.l2()[0], c.l2()[1], c.l2()[2]);
+  Cost cost = Cost::FromDiagonals(p.q0, p.q1, p.q2, p.r0, p.r1);
+  std::printf("\"cost_diag\": [%.17g, %.17g, %.17g, %.17g, %.17g]}\n", cost.q()[0][0], cost.q()[1][1],
+              cost.q()[2][2], cost.r()[0][0], cost.r()[1][1]);
+  return 0;
+}
+
+static int tick(const char* params_path, const char* in, const char* out, bool batch) {
+  Params p;
+  if (!LoadParams(params_path, &p)) return 2;
+  const std::vector<float> d = read_all(in);
+  const int T = static_cast<int>(d[0]), N = static_cast<int>(d[1]);
+  p.horizon = N;
+  MPC mpc(p);
+  if (!mpc.solver_ok()) {
+    std::fprintf(stderr, "%s\n", mpc.last_error().c_str());
+    return 3;
+  }
+  std::vector<float> res;
+  size_t o = 2;
+  if (!batch) {
+    for (int t = 0; t < T; t++) {
+      State x0(d[o], d[o + 1], d[o + 2]);
+      Input ul(d[o + 3], d[o + 4]);
+      o += 5;
+      std::vector<State> xr;
+      for (int i = 0; i < N; i++, o += 3) xr.emplace_back(d[o], d[o + 1], d[o + 2]);
+      mpc.Update(x0, ul, xr);
+      res.push_back(static_cast<float>(mpc.last_status()));
+      for (double z : mpc.solution()) res.push_back(static_cast<float>(z));
+      res.push_back(static_cast<float>(mpc.solved_trajectory().size()));
+    }
+  } else {
+    State x0(d[o], d[o + 1], d[o + 2]);
+    Input ul(d[o + 3], d[o + 4]);
+    o += 5;
+    std::vector<std::vector<State>> cands(T);
+    for (int t = 0; t < T; t++)
+      for (int i = 0; i < N; i++, o += 3) cands[t].emplace_back(d[o], d[o + 1], d[o + 2]);
+    std::vector<float> u, x;
+    const std::vector<int> st = mpc.UpdateBatch(x0, ul, cands, &u, &x);
+    for (int s : st) res.push_back(static_cast<float>(s));
+    res.insert(res.end(), u.begin(), u.end());
+    res.insert(res.end(), x.begin(), x.end());
+  }
+  std::ofstream f(out, std::ios::binary);
+  f.write(reinterpret_cast<const char*>(res.data()), res.size() * 4);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc >= 3 && !std::strcmp(argv[1], "cpu")) return cpu(argv[2]);
+  if (argc >= 5 && !std::strcmp(argv[1], "tick")) return tick(argv[2], argv[3], argv[4], false);
+  if (argc >= 5 && !std::strcmp(argv[1], "batch")) return tick(argv[2], argv[3], argv[4], true);
+  std::fprintf(stderr, "usage: host_demo cpu|tick|batch ...\n");
+  return 1;
+}
