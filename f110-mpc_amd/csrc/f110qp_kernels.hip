@@ -170,7 +170,9 @@ struct Lin {
 __device__ __forceinline__ Lin linearize(double th, double v, double d, float dtf) {
   const double dt = (double)dtf;
   const double L = (double)0.3302f;
-  const double sn = sin(th), cs = cos(th), cd = cos(d);
+  double sn, cs, sd, cd;
+  sincos(th, &sn, &cs);
+  sincos(d, &sd, &cd);
   const double sec2 = 1.0 / (cd * cd);  // pow(cos(d), -2)
   Lin M;
   M.th0 = th;
@@ -178,7 +180,7 @@ __device__ __forceinline__ Lin linearize(double th, double v, double d, float dt
   M.a12 = v * cs * dt;                // :43
   M.b00 = cs * dt;                    // :48
   M.b10 = sn * dt;                    // :49
-  M.b20 = tan(d) * dt / L;            // :50
+  M.b20 = (sd / cd) * dt / L;         // :50 tan(d)
   M.b21 = v * sec2 * dt / L;          // :51
   M.c0 = v * th * sn * dt;            // :53
   M.c1 = -1 * v * th * cs * dt;       // :54
@@ -254,7 +256,9 @@ __device__ __forceinline__ double grad_f64(const Lin& M, const KParams& P, int l
 // ------------------------------------------------------------------------------------------
 template <int NUM>
 struct Smem {
-  float W[NUM][NUM];       // W = H^-1, row-major (symmetric: row p == column p)
+  // first and 16-B aligned: small immediate offsets, ds_read_b128 broadcasts in the sweep
+  alignas(16) float colbuf[2][64];  // sweep: pivot column all-gather (double buffered)
+  alignas(16) float W[NUM][NUM];    // W = H^-1, row-major (symmetric: row p == column p)
   float V[NUM][NUM];       // V[slot][var] = W n_slot
   float S[NUM][NUM + 1];   // S_A = N_A' W N_A
   float L[NUM][NUM + 1];   // Cholesky factor of S_A (lower)
@@ -308,8 +312,16 @@ __device__ __forceinline__ float chol_slots(Smem<NUM>& sm, int lane, int q, floa
   for (int c = 0; c < q; c++) {
     float s = 0.f;
     if (lane < q && lane >= c) {
-      s = sm.S[lane][c];
-      for (int i2 = 0; i2 < c; i2++) s = fmaf(-sm.L[lane][i2], sm.L[c][i2], s);
+      float s0 = sm.S[lane][c], s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      int i2 = 0;
+      for (; i2 + 4 <= c; i2 += 4) {  // four independent chains: the LDS reads pipeline
+        s0 = fmaf(-sm.L[lane][i2 + 0], sm.L[c][i2 + 0], s0);
+        s1 = fmaf(-sm.L[lane][i2 + 1], sm.L[c][i2 + 1], s1);
+        s2 = fmaf(-sm.L[lane][i2 + 2], sm.L[c][i2 + 2], s2);
+        s3 = fmaf(-sm.L[lane][i2 + 3], sm.L[c][i2 + 3], s3);
+      }
+      for (; i2 < c; i2++) s0 = fmaf(-sm.L[lane][i2], sm.L[c][i2], s0);
+      s = (s0 + s1) + (s2 + s3);
     }
     const float dcc = sqrtf(readlane_f(s, c));
     if (lane < q && lane >= c) sm.L[lane][c] = (lane == c) ? dcc : s / dcc;
@@ -344,22 +356,31 @@ __device__ __forceinline__ float slot_dot(Smem<NUM>& sm, int slot_id, float ga0,
 
 // One pivot of the symmetric sweep operator (Goodnight 1979) on the row held by this lane:
 //   a_ij -= a_ip a_pj / a_pp ; a_ip /= a_pp ; a_pj /= a_pp ; a_pp = -1/a_pp.
-// The pivot row is broadcast with readlane; its own update folds into the common FMA with
+// The pivot column is all-gathered through LDS; the pivot row's own update folds into the common FMA with
 // f = 1 - 1/a_pp. After all pivots the rows hold -H^-1. P is a template constant so every
 // register index is static (no scratch).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <int NUM, int P>
-__device__ __forceinline__ void sweep_step(Smem<NUM>&, float (&hrow)[NUM], int lane) {
+__device__ __forceinline__ void sweep_step(Smem<NUM>& sm, float (&hrow)[NUM], int lane) {
   // pivot row broadcast by readlane (lane P, static register index) -> SGPR operands
   float rk[NUM];
 #pragma unroll
   for (int j = 0; j < NUM; j++) rk[j] = readlane_f(hrow[j], P);
-  const float inv = 1.f / rk[P];
+  const float inv = __builtin_amdgcn_rcpf(rk[P]);  // 1 ulp; the fp64 refinement absorbs it
   const bool piv = (lane == P);
-  const float f = piv ? (1.f - inv) : hrow[P] * inv;
+  const float hp = hrow[P];
+  const float f = piv ? (1.f - inv) : hp * inv;
+  const f32x2 nf = {-f, -f};
 #pragma unroll
-  for (int j = 0; j < NUM; j++)
-    if (j != P) hrow[j] = fmaf(-f, rk[j], hrow[j]);
-  hrow[P] = piv ? -inv : hrow[P] * inv;
+  for (int j = 0; j < NUM; j += 2) {  // packed FMA over column pairs (v_pk_fma_f32)
+    const f32x2 r = {rk[j], rk[j + 1]};
+    f32x2 h = {hrow[j], hrow[j + 1]};
+    h = __builtin_elementwise_fma(nf, r, h);
+    hrow[j] = h.x;
+    hrow[j + 1] = h.y;
+  }
+  hrow[P] = piv ? -inv : hp * inv;
 }
 
 template <int NUM, int P>
@@ -508,6 +529,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
 
   STAMP(t_hess);
   // ---- 3. W = H^-1 : symmetric sweep (Goodnight), row `lane` in registers ----------------
+  sm.colbuf[0][lane] = hrow[0];
   Sweep<NUM, 0>::run(sm, hrow, lane);
   if (lane < NUM) {
 #pragma unroll
@@ -549,66 +571,98 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
     constexpr int kPdasMaxIter = 10;
     const float uunc = xv;
     sm.vec[lane] = uunc;
-    int act = 0;  // 0 free, 1 at the lower bound, 2 at the upper bound
+    const int cl = lane < NUM ? lane : NUM - 1;
+    int act = 0;           // 0 free, 1 at the lower bound, 2 at the upper bound
+    int qn = 0;            // slots of the current guess (slot j held by lane j)
+    int svar = 0;          // slot lane: its variable
+    float ssg = 1.f;       // slot lane: +1 lower bound row (n = e), -1 upper bound row (n = -e)
+    float rdp = 0.f;       // slot lane: 1 / L[j][j]
+    bool converged = false;
+    float u = uunc, mu = 0.f;
     for (int pit = 0; pit < kPdasMaxIter; pit++) {
-      const unsigned long long mask = __ballot(act != 0);
-      const int qn = __popcll(mask);
-      const int myslot = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
-      if (act) sm.ids[myslot] = 3 * lane + (act == 2 ? 1 : 0);
-      wsync();
-      const int sid = (lane < qn) ? sm.ids[lane] : 0;
-      const int svar = sid / 3;
-      const float ssg = (sid - 3 * svar == 0) ? 1.f : -1.f;
+      // solve the equality QP of the current slots: mu = S^-1 (b - N'u_unc), u = u_unc + W N mu
       float rhs = 0.f;
       if (lane < qn) {
         const float bj = (ssg > 0.f) ? ((svar & 1) ? umin1 : umin0) : -((svar & 1) ? umax1 : umax0);
-        rhs = bj - ssg * sm.vec[svar];  // b_j - n_j' u_unc
-        for (int l = 0; l < qn; l++) {
-          const int idl = sm.ids[l];
-          const int vl = idl / 3;
-          const float sgl = (idl - 3 * vl == 0) ? 1.f : -1.f;
-          sm.S[lane][l] = ssg * sgl * sm.W[svar][vl];
-        }
+        rhs = bj - ssg * sm.vec[svar];
       }
-      wsync();
-      const float rdp = chol_slots<NUM>(sm, lane, qn, 0.f);
       const float lvp = tri_forward<NUM>(sm, lane, qn, rdp, rhs);
-      const float mu = tri_backward<NUM>(sm, lane, qn, rdp, lvp);
-      // u = u_unc + sum_j mu_j W n_j
-      float u = uunc;
-      const int cl = lane < NUM ? lane : NUM - 1;
-      for (int j = 0; j < qn; j++) {
-        const int vj = readlane_i(svar, j);
-        u = fmaf(readlane_f(mu * ssg, j), sm.W[vj][cl], u);
-      }
+      mu = tri_backward<NUM>(sm, lane, qn, rdp, lvp);
+      u = uunc;
+      for (int j = 0; j < qn; j++) u = fmaf(readlane_f(mu * ssg, j), sm.W[readlane_i(svar, j)][cl], u);
       if (lane < qn) sm.pmu[svar] = mu;
       wsync();
       const float myu = act ? sm.pmu[lane] : 0.f;
       const bool nlo = valid && ((act == 1 ? myu : 0.f) + (lb - u) > 0.f);
       const bool nhi = valid && !nlo && ((act == 2 ? myu : 0.f) + (u - ub) > 0.f);
       const int nact = nlo ? 1 : (nhi ? 2 : 0);
-      const bool changed = __ballot(nact != act) != 0;
-      wsync();
-      if (!changed) {
-        // converged: hand the active set to the GI state
-        q = qn;
-        slot_id = (lane < qn) ? sid : -1;
-        mult = (lane < qn) ? fmaxf(mu, 0.f) : 0.f;
-        rdiag = (lane < qn) ? rdp : 0.f;
-        actf = act;  // bit0 lower, bit1 upper
-        if (lane < NUM)
-          for (int j = 0; j < qn; j++) {
-            const int idj = sm.ids[j];
-            const int vj = idj / 3;
-            sm.V[j][lane] = ((idj - 3 * vj == 0) ? 1.f : -1.f) * sm.W[vj][lane];
-          }
-        xv = valid ? u : 0.f;
-        it = pit + 1;
+      const unsigned long long changed = __ballot(nact != act);
+      if (!changed) { converged = true; it = pit + 1; break; }
+      if (__ballot(act != 0 && nact != act)) {
+        // a slot leaves (or flips side): rebuild slots and chol(S_A) from the new set
+        const unsigned long long mask = __ballot(nact != 0);
+        qn = __popcll(mask);
+        const int myslot = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
+        if (nact) sm.ids[myslot] = 3 * lane + (nact == 2 ? 1 : 0);
         wsync();
-        break;
+        const int sid = (lane < qn) ? sm.ids[lane] : 0;
+        svar = sid / 3;
+        ssg = (sid - 3 * svar == 0) ? 1.f : -1.f;
+        if (lane < qn)
+          for (int l = 0; l < qn; l++) {
+            const int idl = sm.ids[l];
+            const int vl = idl / 3;
+            sm.S[lane][l] = ssg * ((idl - 3 * vl == 0) ? 1.f : -1.f) * sm.W[svar][vl];
+          }
+        wsync();
+        rdp = chol_slots<NUM>(sm, lane, qn, 0.f);
+      } else {
+        // only additions: append each new bound as a slot with one forward solve
+        // (incremental Cholesky row l = L^-1 S[q][:q], L[q][q] = sqrt(S[q][q] - l'l))
+        unsigned long long addm = changed;
+        while (addm) {
+          const int v = __builtin_ctzll(addm);
+          addm &= addm - 1;
+          const int na = readlane_i(nact, v);
+          const float sg = (na == 1) ? 1.f : -1.f;
+          const float sv = (lane < qn) ? sg * ssg * sm.W[v][svar] : 0.f;
+          const float lrow = tri_forward<NUM>(sm, lane, qn, rdp, sv);
+          const float ll = wave_sum(lane < qn ? lrow * lrow : 0.f);
+          const float dnew = sqrtf(sm.W[v][v] - ll);
+          if (lane < qn) sm.L[qn][lane] = lrow;
+          if (lane == qn) {
+            sm.L[qn][qn] = dnew;
+            svar = v;
+            ssg = sg;
+            rdp = 1.f / dnew;
+          }
+          if (lane == 0) sm.ids[qn] = 3 * v + (na == 2 ? 1 : 0);
+          qn++;
+          wsync();
+        }
       }
       act = nact;
+    }
+    if (converged) {
+      // hand the active set to the GI state: slots, multipliers, W n_j, S_A, chol(S_A)
+      q = qn;
+      slot_id = (lane < qn) ? 3 * svar + (ssg > 0.f ? 0 : 1) : -1;
+      mult = (lane < qn) ? fmaxf(mu, 0.f) : 0.f;
+      rdiag = (lane < qn) ? rdp : 0.f;
+      actf = act;  // bit0 lower, bit1 upper
+      if (lane < NUM)
+        for (int j = 0; j < qn; j++) {
+          const int vj = readlane_i(svar, j);
+          sm.V[j][lane] = readlane_f(ssg, j) * sm.W[vj][lane];
+        }
+      if (lane < qn)
+        for (int l = 0; l < qn; l++) {
+          const int vl = readlane_i(svar, l);
+          sm.S[lane][l] = ssg * readlane_f(ssg, l) * sm.W[svar][vl];
+        }
+      xv = valid ? u : 0.f;
+      wsync();
     }
     STAMP_ACC(acc_pdas, t_pdas);
   }
@@ -709,6 +763,12 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
           mult += du;
           wsync();
           if (lane < q) sm.cmult[slot_id] = mult;
+          // a second step only if the first correction was not already at fp32 noise level
+          float adx = valid ? fabsf(dx) : 0.f;
+          int dummy = 0;
+          adx = -adx;
+          wave_argmin(adx, dummy);  // -max |dx|
+          if (-adx <= 1e-5f) break;
         }
         wsync();
         // fp64 feasibility check of every inactive row at the refined point
