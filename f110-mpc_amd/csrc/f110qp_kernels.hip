@@ -485,36 +485,56 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
 
   STAMP(t_grad);
   // ---- 2b. condensed Hessian row (closed form, fp32) --------------------------------------
+  // Row v = (k, a), column w = (l, b). For l <= k the stages that see both inputs are
+  // i = k+1..N (T = N-k of them), and Gamma_i[:, w] is affine in the stage distance, so
+  //   H[v][w] = C0_b + C1_b * (k - l)
+  // with four per-lane constants (sums of 1, t, t^2 over the T stages). The entries with
+  // l > k are the transpose: every lane publishes its lower row and reads column v back.
   float hrow[NUM];
   {
     const Lin M = sm.M;
     const float fa02 = (float)M.a02, fa12 = (float)M.a12, fb00 = (float)M.b00;
     const float fb10 = (float)M.b10, fb20 = (float)M.b20, fb21 = (float)M.b21;
-    const float beta_a = a ? fb21 : fb20;
-    const float ax_a = a ? 0.f : fb00, ay_a = a ? 0.f : fb10;
     const float q0 = (float)P.q[0], q1 = (float)P.q[1], q2 = (float)P.q[2];
     const float ra = a ? (float)P.r[1] : (float)P.r[0];
+    const float T = (float)(N - k);
+    const float S1 = T * (T - 1.f) * 0.5f;
+    const float S2 = (T - 1.f) * T * (2.f * T - 1.f) * (1.f / 6.f);
+    const float beta_a = a ? fb21 : fb20;
+    const float pxa = a ? 0.f : fb00, pya = a ? 0.f : fb10;  // dk = 0 in this regime
+    const float sxa = fa02 * beta_a, sya = fa12 * beta_a;
+    const float Ux = T * pxa + sxa * S1, Vx = pxa * S1 + sxa * S2;
+    const float Uy = T * pya + sya * S1, Vy = pya * S1 + sya * S2;
+    float C0[2], C1[2];
+#pragma unroll
+    for (int bb = 0; bb < 2; bb++) {
+      const float beta_b = bb ? fb21 : fb20;
+      const float ax_b = bb ? 0.f : fb00, ay_b = bb ? 0.f : fb10;
+      const float sxb = fa02 * beta_b, syb = fa12 * beta_b;
+      C0[bb] = q0 * (ax_b * Ux + sxb * Vx) + q1 * (ay_b * Uy + syb * Vy) + q2 * T * beta_a * beta_b;
+      C1[bb] = q0 * sxb * Ux + q1 * syb * Uy;
+    }
+    float lower[NUM];
 #pragma unroll
     for (int w = 0; w < NUM; w++) {
       const int l = w >> 1, bb = w & 1;
-      const float beta_b = bb ? fb21 : fb20;
-      const float ax_b = bb ? 0.f : fb00, ay_b = bb ? 0.f : fb10;
-      const int m = k > l ? k : l;
-      const float T = (float)(N - m);
-      const float S1 = T * (T - 1.f) * 0.5f;
-      const float S2 = (T - 1.f) * T * (2.f * T - 1.f) * (1.f / 6.f);
-      const float dk = (float)(m - k), dl = (float)(m - l);
-      const float sxa = fa02 * beta_a, sxb = fa02 * beta_b;
-      const float sya = fa12 * beta_a, syb = fa12 * beta_b;
-      const float pxa = ax_a + sxa * dk, pxb = ax_b + sxb * dl;
-      const float pya = ay_a + sya * dk, pyb = ay_b + syb * dl;
-      const float hx = T * pxa * pxb + (pxa * sxb + pxb * sxa) * S1 + sxa * sxb * S2;
-      const float hy = T * pya * pyb + (pya * syb + pyb * sya) * S1 + sya * syb * S2;
-      float h = q0 * hx + q1 * hy + q2 * T * beta_a * beta_b;
+      lower[w] = fmaf(C1[bb], (float)(k - l), C0[bb]);
+    }
+    if (lane < NUM) {
+#pragma unroll
+      for (int w = 0; w < NUM; w++) sm.W[lane][w] = lower[w];
+    }
+    wsync();
+    const int cl = lane < NUM ? lane : NUM - 1;
+#pragma unroll
+    for (int w = 0; w < NUM; w++) {
+      const int l = w >> 1;
+      float h = (l <= k) ? lower[w] : sm.W[w][cl];
       if (w == lane) h += ra;
       const bool ok = valid && (w < NU);
       hrow[w] = ok ? h : (w == lane ? 1.f : 0.f);
     }
+    wsync();
   }
   if (Hdbg) {  // debug/parity hook: dump H (g was written above), no solve
     if (valid) {
@@ -598,8 +618,8 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
       const int nact = nlo ? 1 : (nhi ? 2 : 0);
       const unsigned long long changed = __ballot(nact != act);
       if (!changed) { converged = true; it = pit + 1; break; }
-      if (__ballot(act != 0 && nact != act)) {
-        // a slot leaves (or flips side): rebuild slots and chol(S_A) from the new set
+      if (qn == 0 || __ballot(act != 0 && nact != act)) {
+        // first guess, or a slot leaves / flips side: build slots and chol(S_A) from scratch
         const unsigned long long mask = __ballot(nact != 0);
         qn = __popcll(mask);
         const int myslot = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
