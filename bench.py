@@ -26,21 +26,27 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "f110-mpc_amd"))
 
 CONFIGS = {
-    # name: (batch per GPU, horizon, gap rows active, description)
-    "c2": (1024, 20, False, "configs[1]: batch=1024 QPs, horizon=20, box constraints only"),
-    "c3": (4096, 20, True, "configs[2]: batch=4096 QPs, horizon=20, + half-space gap constraints"),
-    "c2_big": (65536, 20, False, "throughput: batch=65536 QPs, horizon=20, box constraints"),
+    # name: (batch per GPU, horizon, gap rows active, warm-started stream, description)
+    "c2": (1024, 20, False, False, "configs[1]: batch=1024 QPs, horizon=20, box constraints only"),
+    "c3": (4096, 20, True, False, "configs[2]: batch=4096 QPs, horizon=20, + half-space gap constraints"),
+    "c5": (4096, 20, False, True, "configs[4]: batch=4096 QPs, horizon=20, warm-started receding-horizon "
+                                   "stream (x0 advances 4.5*dt per step, KKT factor reused)"),
+    "c5_cold": (4096, 20, False, False, "configs[4] stream solved cold (no warm start), for comparison"),
+    "c2_big": (65536, 20, False, False, "throughput: batch=65536 QPs, horizon=20, box constraints"),
 }
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
 
 
-def bytes_per_qp(N: int, gap: bool) -> int:
-    """ABI bytes moved per QP: x0, u_lin, x_ref (+ halfspace) in; u*, x*, status, iters out."""
+def bytes_per_qp(N: int, gap: bool, warm: bool = False) -> int:
+    """ABI bytes moved per QP: x0, u_lin, x_ref (+ halfspace) in; u*, x*, status, iters out;
+    warm start adds the slot key and active masks (read + write) and one read of the cached
+    W = H^-1 (2N x 2N fp32) on a key hit."""
     inp = 4 * (3 + 2 + 3 * N + (6 if gap else 0))
     out = 4 * (2 * N + 3 * (N + 1) + 1 + 1)
-    return inp + out
+    extra = (2 * 32 + 4 * (2 * N) ** 2) if warm else 0
+    return inp + out + extra
 
 
 def flops_per_qp(N: int, mean_iters: float, mean_active: float) -> float:
@@ -131,10 +137,20 @@ def main():
 
     from f110qp import capi, workload
 
-    Bper, N, gap, desc = CONFIGS[args.config]
+    Bper, N, gap, warm, desc = CONFIGS[args.config]
     if args.batch:
         Bper = args.batch
-    w = workload.make_batch(Bper, N, seed=1000 + rank)
+    stream_cfg = args.config.startswith("c5")
+    if stream_cfg:
+        # one tick of the stream per step, all ticks staged in HBM before timing
+        nt = args.warmup + args.steps + 20
+        ticks = workload.make_stream(Bper, N, nt, seed=1000 + rank)
+        X0 = torch.from_numpy(np.stack([t["x0"] for t in ticks])).to(dev)
+        UL = torch.from_numpy(np.stack([t["u_lin"] for t in ticks])).to(dev)
+        XR = torch.from_numpy(np.stack([t["x_ref"] for t in ticks])).to(dev)
+        w = ticks[0]
+    else:
+        w = workload.make_batch(Bper, N, seed=1000 + rank)
     x0 = torch.from_numpy(w["x0"]).to(dev)
     ul = torch.from_numpy(w["u_lin"]).to(dev)
     xr = torch.from_numpy(w["x_ref"]).to(dev)
@@ -147,12 +163,19 @@ def main():
     xo = torch.empty((Bper, N + 1, 3), dtype=torch.float32, device=dev)
     st = torch.empty((Bper,), dtype=torch.int32, device=dev)
     it = torch.empty((Bper,), dtype=torch.int32, device=dev)
-    cfg = capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, device=dev.index)
+    cfg = capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, device=dev.index,
+                              warm_start=int(warm))
     solver = capi.Solver(cfg)
     stream = torch.cuda.current_stream(dev)
+    tick = [0]
 
     def step():
-        solver.solve_dev(x0, ul, xr, hs, uo, xo, st, it, stream=stream)
+        if stream_cfg:
+            t = tick[0]
+            tick[0] += 1
+            solver.solve_dev(X0[t], UL[t], XR[t], hs, uo, xo, st, it, stream=stream)
+        else:
+            solver.solve_dev(x0, ul, xr, hs, uo, xo, st, it, stream=stream)
 
     for _ in range(args.warmup):
         step()
@@ -179,7 +202,7 @@ def main():
 
     # dominant kernel duration: HIP events around single launches on the launch stream
     evs = []
-    for _ in range(20):
+    for _ in range(20 if not stream_cfg else 18):
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         a.record(stream)
@@ -192,7 +215,7 @@ def main():
     total_qps = Bper * world * args.steps
     value = total_qps / el
     ms_per_step = el / args.steps * 1e3
-    bpq = bytes_per_qp(N, gap)
+    bpq = bytes_per_qp(N, gap, warm)
     # active-set size ~ iterations for an add-only run; use iterations as the upper bound
     fpq = flops_per_qp(N, float(itn.mean()), float(itn.mean()))
     achieved_gbs = bpq * Bper / (kms * 1e-3) / 1e9
@@ -218,6 +241,7 @@ def main():
             "global_batch": Bper * world,
             "horizon": N,
             "gap_rows": bool(gap),
+            "warm_start": bool(warm),
             "parallelism": f"independent QP shards x{world} (no collective)",
             "solved_fraction": solved,
             "mean_active_set_iters": float(itn.mean()),

@@ -54,6 +54,8 @@ struct f110qp_ctx {
   f110qp_config cfg;
   f110qp::KParams kp;
   DevBuf x0, ul, xr, hs, uo, xo, st, it;
+  DevBuf wW, wkey, wact;  // warm-start slot state (config.warm_start)
+  int warm_batch = 0;     // batch size the warm state was laid out for
   hipStream_t stream = nullptr;
 };
 
@@ -76,6 +78,7 @@ void f110qp_default_config(f110qp_config* c, int horizon) {
   c->gap_mode = F110QP_GAP_INACTIVE;
   c->max_iter = 0;
   c->device = 0;
+  c->warm_start = 0;
 }
 
 static int validate_config(const f110qp_config* c) {
@@ -92,6 +95,7 @@ static int validate_config(const f110qp_config* c) {
   if (c->gap_mode != F110QP_GAP_INACTIVE && c->gap_mode != F110QP_GAP_ACTIVE)
     return fail(F110QP_ERR_INVALID, "gap_mode must be F110QP_GAP_INACTIVE or F110QP_GAP_ACTIVE");
   if (c->max_iter < 0) return fail(F110QP_ERR_INVALID, "max_iter must be >= 0");
+  if (c->warm_start != 0 && c->warm_start != 1) return fail(F110QP_ERR_INVALID, "warm_start must be 0 or 1");
   return F110QP_OK;
 }
 
@@ -123,6 +127,7 @@ void f110qp_destroy(f110qp_ctx* c) {
   if (!c) return;
   c->x0.release(); c->ul.release(); c->xr.release(); c->hs.release();
   c->uo.release(); c->xo.release(); c->st.release(); c->it.release();
+  c->wW.release(); c->wkey.release(); c->wact.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -141,13 +146,42 @@ static int check_batch_args(f110qp_ctx* c, int batch, const void* x0, const void
   return F110QP_OK;
 }
 
+// Warm-start slot state for a batch of `batch` QPs (allocated and zeroed on first use and
+// whenever the batch size changes; zero keys = no valid entry).
+static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState* ws) {
+  *ws = f110qp::WarmState();
+  if (!c->cfg.warm_start) return F110QP_OK;
+  const size_t B = (size_t)batch, nu = 2 * (size_t)c->cfg.horizon;
+  hipError_t e;
+  if ((e = c->wW.ensure(B * nu * nu * 4)) || (e = c->wkey.ensure(B * 16)) || (e = c->wact.ensure(B * 16)))
+    return hip_fail(e, "hipMalloc warm-start state");
+  if (c->warm_batch != batch) {
+    if ((e = hipMemsetAsync(c->wkey.p, 0, B * 16, s)) || (e = hipMemsetAsync(c->wact.p, 0, B * 16, s)))
+      return hip_fail(e, "hipMemsetAsync warm-start state");
+    c->warm_batch = batch;
+  }
+  ws->W = (float*)c->wW.p;
+  ws->key = (unsigned*)c->wkey.p;
+  ws->act = (unsigned long long*)c->wact.p;
+  return F110QP_OK;
+}
+
+int f110qp_warm_reset(f110qp_ctx* c) {
+  if (!c) return fail(F110QP_ERR_INVALID, "ctx is NULL");
+  c->warm_batch = 0;  // the next call re-zeroes the slot keys
+  return F110QP_OK;
+}
+
 int f110qp_solve_batch_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                            const float* xr, const float* hs, float* uo, float* xo, int* st,
                            int* it, void* stream) {
   int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
   if (rc || batch == 0) return rc;
   const float* h = (c->cfg.gap_mode == F110QP_GAP_ACTIVE) ? hs : nullptr;
-  hipError_t e = f110qp::launch_solve(c->kp, batch, x0, ul, xr, h, uo, xo, st, it,
+  f110qp::WarmState ws;
+  rc = warm_state(c, batch, (hipStream_t)stream, &ws);
+  if (rc) return rc;
+  hipError_t e = f110qp::launch_solve(c->kp, batch, x0, ul, xr, h, uo, xo, st, it, ws,
                                       (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
   return F110QP_OK;
@@ -179,9 +213,12 @@ int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* u
       (e = hipMemcpyAsync(c->xr.p, xr, s_xr, hipMemcpyHostToDevice, s)) ||
       (gap && (e = hipMemcpyAsync(c->hs.p, hs, s_hs, hipMemcpyHostToDevice, s))))
     return hip_fail(e, "hipMemcpyAsync H2D");
+  f110qp::WarmState ws;
+  rc = warm_state(c, batch, s, &ws);
+  if (rc) return rc;
   e = f110qp::launch_solve(c->kp, batch, (const float*)c->x0.p, (const float*)c->ul.p,
                            (const float*)c->xr.p, gap ? (const float*)c->hs.p : nullptr,
-                           (float*)c->uo.p, (float*)c->xo.p, (int*)c->st.p, (int*)c->it.p, s);
+                           (float*)c->uo.p, (float*)c->xo.p, (int*)c->st.p, (int*)c->it.p, ws, s);
   if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
   if ((e = hipMemcpyAsync(uo, c->uo.p, s_uo, hipMemcpyDeviceToHost, s)) ||
       (e = hipMemcpyAsync(xo, c->xo.p, s_xo, hipMemcpyDeviceToHost, s)) ||

@@ -23,10 +23,21 @@ struct KParams {
   int max_iter;   // active-set iteration cap
 };
 
+// Warm-start state of a context (all null = cold solve). Per QP slot b of the batch:
+//   W[b]   the cached W = H^-1 (2N x 2N, fp32) of the last solve of slot b,
+//   key[b] the float bits of (theta0, v_lin, delta_lin) it was built for + a valid flag,
+//   act[b] the active bounds at the last solution (bit v of act[2b]: lower, act[2b+1]: upper).
+// H depends only on the linearisation point (model.cpp:30-59), so a key hit reuses W exactly.
+struct WarmState {
+  float* W = nullptr;
+  unsigned* key = nullptr;
+  unsigned long long* act = nullptr;
+};
+
 // Solve B QPs. hs == nullptr -> box-only kernel (gap rows inactive).
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u_lin,
                         const float* x_ref, const float* hs, float* u_out, float* x_out,
-                        int* status, int* iters, hipStream_t stream);
+                        int* status, int* iters, const WarmState& warm, hipStream_t stream);
 
 // Dump the condensed H (B x 2N x 2N) and g (B x 2N) as built by the solve kernel.
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* u_lin,

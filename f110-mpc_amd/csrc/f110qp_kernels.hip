@@ -35,9 +35,11 @@ namespace f110qp {
 constexpr int kStampSlots = 16;
 __device__ unsigned long long g_stamps[65536 * kStampSlots];
 #define STAMP(var) unsigned long long var = __builtin_amdgcn_s_memtime()
+#define STAMP_SET(var) var = __builtin_amdgcn_s_memtime()
 #define STAMP_ACC(acc, since) acc += __builtin_amdgcn_s_memtime() - (since)
 #else
 #define STAMP(var)
+#define STAMP_SET(var)
 #define STAMP_ACC(acc, since)
 #endif
 
@@ -409,7 +411,8 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
                                                    int* __restrict__ status_out,
                                                    int* __restrict__ iters_out,
                                                    double* __restrict__ Hdbg,
-                                                   double* __restrict__ gdbg) {
+                                                   double* __restrict__ gdbg,
+                                                   const WarmState ws) {
   __shared__ Smem<NUM> sm;
   const int b = blockIdx.x;
   if (b >= B) return;
@@ -463,6 +466,15 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
   }
   wsync();
 
+  // warm start: does the cached W of this slot belong to the same linearisation point?
+  const bool warm = ws.W != nullptr && Hdbg == nullptr;
+  bool whit = false, wvalid = false;
+  if (warm) {
+    const unsigned* kk = ws.key + 4 * b;
+    wvalid = kk[3] == 1u;
+    whit = wvalid && kk[0] == __float_as_uint(fTH0) && kk[1] == __float_as_uint(ulg[2 * b + 0]) &&
+           kk[2] == __float_as_uint(ulg[2 * b + 1]);
+  }
   STAMP(t_lin);
   // ---- 2a. gradient at u = 0 (fp64 adjoint) and the free response ------------------------
   float cgap = 0.f, gnorm = 1.f;
@@ -484,6 +496,23 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
   }
 
   STAMP(t_grad);
+  STAMP(t_hess);
+  STAMP(t_inv);
+  if (whit) {
+    // ---- 2b/3 (warm hit): W from the slot cache, no Hessian, no sweep ------------------
+    const float g32w = sm.vec[lane];
+    const float* Wc = ws.W + (size_t)b * NU * NU;
+    const int cl = lane < NUM ? lane : NUM - 1;
+#pragma unroll 4
+    for (int j = 0; j < NUM; j++) {
+      float wv = (j == lane) ? 1.f : 0.f;
+      if (j < NU && valid) wv = Wc[(size_t)j * NU + lane];
+      if (lane < NUM) sm.W[j][cl] = wv;
+    }
+    wsync();
+    sm.vec[lane] = g32w;
+    wsync();
+  } else {
   // ---- 2b. condensed Hessian row (closed form, fp32) --------------------------------------
   // Row v = (k, a), column w = (l, b). For l <= k the stages that see both inputs are
   // i = k+1..N (T = N-k of them), and Gamma_i[:, w] is affine in the stage distance, so
@@ -546,8 +575,7 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
   }
   const float g32 = sm.vec[lane];
   wsync();
-
-  STAMP(t_hess);
+  STAMP_SET(t_hess);
   // ---- 3. W = H^-1 : symmetric sweep (Goodnight), row `lane` in registers ----------------
   sm.colbuf[0][lane] = hrow[0];
   Sweep<NUM, 0>::run(sm, hrow, lane);
@@ -556,12 +584,26 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
     for (int j = 0; j < NUM; j++) sm.W[lane][j] = -hrow[j];  // the sweep leaves -H^-1
   }
   wsync();
-
-  STAMP(t_inv);
-  // ---- 4. dual active set (Goldfarb-Idnani, range space) ---------------------------------
-  // x = -W g
   sm.vec[lane] = g32;
+  if (warm) {  // prime the slot cache (coalesced: lane v writes column v of every row)
+    float* Wc = ws.W + (size_t)b * NU * NU;
+    const int cl = lane < NUM ? lane : NUM - 1;
+    for (int j = 0; j < NU; j++)
+      if (valid) Wc[(size_t)j * NU + lane] = sm.W[j][cl];
+    if (lane == 0) {
+      unsigned* kk = ws.key + 4 * b;
+      kk[0] = __float_as_uint(fTH0);
+      kk[1] = __float_as_uint(ulg[2 * b + 0]);
+      kk[2] = __float_as_uint(ulg[2 * b + 1]);
+      kk[3] = 1u;
+    }
+  }
   wsync();
+  }  // !whit
+
+  STAMP_SET(t_inv);
+  // ---- 4. dual active set (Goldfarb-Idnani, range space) ---------------------------------
+  // x = -W g  (g in sm.vec)
   float xv = valid ? -matvec_W<NUM>(sm, lane) : 0.f;
   wsync();
 
@@ -593,13 +635,38 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
     sm.vec[lane] = uunc;
     const int cl = lane < NUM ? lane : NUM - 1;
     int act = 0;           // 0 free, 1 at the lower bound, 2 at the upper bound
+    if (warm && wvalid && valid) {  // previous tick's active bounds seed the first guess
+      const unsigned long long lo_m = ws.act[2 * b], hi_m = ws.act[2 * b + 1];
+      act = ((lo_m >> lane) & 1ull) ? 1 : (((hi_m >> lane) & 1ull) ? 2 : 0);
+    }
     int qn = 0;            // slots of the current guess (slot j held by lane j)
     int svar = 0;          // slot lane: its variable
     float ssg = 1.f;       // slot lane: +1 lower bound row (n = e), -1 upper bound row (n = -e)
     float rdp = 0.f;       // slot lane: 1 / L[j][j]
     bool converged = false;
     float u = uunc, mu = 0.f;
+    bool seeded = __ballot(act != 0) != 0;  // warm guess: build its slots before the first solve
     for (int pit = 0; pit < kPdasMaxIter; pit++) {
+      if (seeded) {
+        seeded = false;
+        const unsigned long long mask = __ballot(act != 0);
+        qn = __popcll(mask);
+        const int myslot = __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
+        if (act) sm.ids[myslot] = 3 * lane + (act == 2 ? 1 : 0);
+        wsync();
+        const int sid = (lane < qn) ? sm.ids[lane] : 0;
+        svar = sid / 3;
+        ssg = (sid - 3 * svar == 0) ? 1.f : -1.f;
+        if (lane < qn)
+          for (int l = 0; l < qn; l++) {
+            const int idl = sm.ids[l];
+            const int vl = idl / 3;
+            sm.S[lane][l] = ssg * ((idl - 3 * vl == 0) ? 1.f : -1.f) * sm.W[svar][vl];
+          }
+        wsync();
+        rdp = chol_slots<NUM>(sm, lane, qn, 0.f);
+      }
       // solve the equality QP of the current slots: mu = S^-1 (b - N'u_unc), u = u_unc + W N mu
       float rhs = 0.f;
       if (lane < qn) {
@@ -972,6 +1039,14 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
     status_out[b] = status;
     if (iters_out) iters_out[b] = it;
   }
+  if (warm) {
+    const unsigned long long lo_m = __ballot(ok && valid && (actf & 1));
+    const unsigned long long hi_m = __ballot(ok && valid && (actf & 2));
+    if (lane == 0) {
+      ws.act[2 * b] = lo_m;
+      ws.act[2 * b + 1] = hi_m;
+    }
+  }
 #ifdef F110QP_STAMPS
   STAMP(t_end);
   if (lane == 0 && b < 65536) {
@@ -991,41 +1066,41 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
 template <int NUM, bool GAP>
 static hipError_t launch_t(const KParams& P, int B, const float* x0, const float* ul,
                            const float* xr, const float* hs, float* uo, float* xo, int* st,
-                           int* its, double* Hd, double* gd, hipStream_t s) {
+                           int* its, double* Hd, double* gd, const WarmState& ws, hipStream_t s) {
   hipLaunchKernelGGL((solve_kernel<NUM, GAP>), dim3(B), dim3(64), 0, s, P, B, x0, ul, xr, hs, uo,
-                     xo, st, its, Hd, gd);
+                     xo, st, its, Hd, gd, ws);
   return hipGetLastError();
 }
 
 template <bool GAP>
 static hipError_t launch_g(const KParams& P, int B, const float* x0, const float* ul,
                            const float* xr, const float* hs, float* uo, float* xo, int* st,
-                           int* its, double* Hd, double* gd, hipStream_t s) {
+                           int* its, double* Hd, double* gd, const WarmState& ws, hipStream_t s) {
   const int NU = 2 * P.N;
-  if (NU <= 8) return launch_t<8, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, s);
-  if (NU <= 16) return launch_t<16, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, s);
-  if (NU <= 24) return launch_t<24, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, s);
-  if (NU <= 32) return launch_t<32, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, s);
-  if (NU <= 40) return launch_t<40, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, s);
-  if (NU <= 48) return launch_t<48, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, s);
-  if (NU <= 56) return launch_t<56, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, s);
-  if (NU <= 64) return launch_t<64, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, s);
+  if (NU <= 8) return launch_t<8, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, s);
+  if (NU <= 16) return launch_t<16, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, s);
+  if (NU <= 24) return launch_t<24, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, s);
+  if (NU <= 32) return launch_t<32, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, s);
+  if (NU <= 40) return launch_t<40, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, s);
+  if (NU <= 48) return launch_t<48, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, s);
+  if (NU <= 56) return launch_t<56, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, s);
+  if (NU <= 64) return launch_t<64, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, s);
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
                         const float* xr, const float* hs, float* uo, float* xo, int* st,
-                        int* its, hipStream_t s) {
+                        int* its, const WarmState& ws, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (hs) return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, s);
-  return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, s);
+  if (hs) return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, s);
+  return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, s);
 }
 
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* ul,
                                  const float* xr, double* Hd, double* gd, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   return launch_g<false>(P, B, x0, ul, xr, nullptr, nullptr, nullptr, nullptr, nullptr, Hd, gd,
-                         s);
+                         WarmState(), s);
 }
 
 }  // namespace f110qp

@@ -37,6 +37,7 @@ EXPORTED = (
     "f110qp_solve_batch",
     "f110qp_solve_batch_dev",
     "f110qp_condense_debug_dev",
+    "f110qp_warm_reset",
     "f110qp_find_half_spaces",
     "f110qp_find_half_spaces_dev",
 )
@@ -54,6 +55,7 @@ class Config(C.Structure):
         ("gap_mode", C.c_int),
         ("max_iter", C.c_int),
         ("device", C.c_int),
+        ("warm_start", C.c_int),
     ]
 
 
@@ -81,6 +83,7 @@ def load():
     L.f110qp_solve_batch.argtypes = [C.c_void_p, C.c_int] + [fp] * 8
     L.f110qp_solve_batch_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 9
     L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
+    L.f110qp_warm_reset.argtypes = [C.c_void_p]
     L.f110qp_find_half_spaces.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_float), C.c_int,
                                           C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
                                           C.c_float, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -174,6 +177,9 @@ class Solver:
         _check(self.lib.f110qp_solve_batch_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
                                                _tp(u_out), _tp(x_out), _tp(status), _tp(iters),
                                                C.c_void_p(stream.cuda_stream)), "f110qp_solve_batch_dev")
+
+    def warm_reset(self):
+        _check(self.lib.f110qp_warm_reset(self._h), "f110qp_warm_reset")
 
     def condense_debug_dev(self, x0, u_lin, x_ref, H_out, g_out, stream=None):
         import torch

@@ -110,3 +110,24 @@ def make_scans(batch: int, seed: int = 0, beams: int = SCAN_BEAMS, gap_center=0.
     m = np.abs(ang[None, :] - ctr[:, None]) < (w[:, None] / 2)
     r[m] = rng.uniform(4.0, 10.0, int(m.sum())).astype(np.float32)
     return r, amin, ainc, amax
+
+
+def make_stream(batch: int, horizon: int, ticks: int, seed: int = 0, dt: float = 0.01, heading_change_every: int = 0):
+    """Config C5: `ticks` consecutive control ticks of `batch` independent cars. Each car keeps
+    its mini path (the reference re-plans only near the path end, src/project.cpp:180-188)
+    while x0 advances 4.5*dt along the heading per tick; u_lin keeps v = 4.5 and the steer of
+    the previous tick. With heading_change_every = k > 0 a tenth of the cars also turn by a
+    small angle every k ticks (their linearisation point changes). Returns a list of dicts."""
+    base = make_batch(batch, horizon, seed=seed)
+    rng = np.random.default_rng(seed + 17)
+    x0 = base["x0"].astype(np.float64).copy()
+    ticks_out = []
+    turners = rng.random(batch) < 0.1
+    for t in range(ticks):
+        if t > 0:
+            x0[:, 0] += SPEED * dt * np.cos(x0[:, 2])
+            x0[:, 1] += SPEED * dt * np.sin(x0[:, 2])
+            if heading_change_every and t % heading_change_every == 0:
+                x0[turners, 2] += rng.uniform(-0.05, 0.05, int(turners.sum()))
+        ticks_out.append(dict(x0=x0.astype(np.float32), u_lin=base["u_lin"].copy(), x_ref=base["x_ref"].copy()))
+    return ticks_out

@@ -73,6 +73,11 @@ typedef struct {
   int gap_mode;     /* F110QP_GAP_INACTIVE | F110QP_GAP_ACTIVE                            */
   int max_iter;     /* active-set iteration cap per QP (0 = default 8*(2N+2N))             */
   int device;       /* HIP device ordinal used by the host-pointer entry points            */
+  int warm_start;   /* 1: keep per-slot state across calls (OsqpEigen setWarmStart(true),   */
+                    /*    mpc.cpp:98): the factor W = H^-1 is reused when a slot's          */
+                    /*    linearisation point (theta0, v, steer) is bit-identical to its    */
+                    /*    previous call's, and the previous active set seeds the solve.    */
+                    /*    Slot b of call t+1 continues slot b of call t (same batch size). */
 } f110qp_config;
 
 /* Library / ABI version (F110QP_API_VERSION). */
@@ -101,6 +106,9 @@ int f110qp_solve_batch(f110qp_ctx* ctx, int batch, const float* x0, const float*
 int f110qp_solve_batch_dev(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
                            const float* x_ref, const float* halfspace, float* u_out,
                            float* x_out, int* status, int* iters, void* stream);
+
+/* Forget the warm-start state of every slot (the next call solves cold). */
+int f110qp_warm_reset(f110qp_ctx* ctx);
 
 /* Debug/parity hook: the condensed Hessian H [B][2N][2N] and gradient g [B][2N] exactly as
  * the solve kernel builds them on the device (float64), for comparison with the CPU oracle's

@@ -267,3 +267,52 @@ def test_large_batch_throughput_shape(oracle, capi):
     idx = np.arange(0, B, 61)
     ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
     assert rel_err(u[idx], ur).max() <= TOL and rel_err(x[idx], xr).max() <= TOL
+
+
+def test_warm_started_stream(oracle, capi):
+    """Config C5: a receding-horizon stream solved with warm_start = 1 (OsqpEigen
+    setWarmStart(true), mpc.cpp:98). Slots whose linearisation point is unchanged reuse the
+    cached W; a tenth of the cars turn every 3 ticks (cache misses). Every tick must equal the
+    exact optimum, and the warm solve must not need more active-set passes than the cold one."""
+    N, B, T = 20, 512, 7
+    stream = workload.make_stream(B, N, T, seed=11, heading_change_every=3)
+    warm = capi.Solver(capi.default_config(N, warm_start=1))
+    cold = capi.Solver(capi.default_config(N))
+    it_w, it_c = [], []
+    for t, w in enumerate(stream):
+        uw, xw, sw, iw = warm.solve(w["x0"], w["u_lin"], w["x_ref"])
+        uc, xc, sc, ic = cold.solve(w["x0"], w["u_lin"], w["x_ref"])
+        ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"])
+        np.testing.assert_array_equal(sw, sr)
+        assert rel_err(uw, ur).max() <= TOL and rel_err(xw, xr).max() <= TOL, t
+        assert rel_err(uc, ur).max() <= TOL
+        if t > 0:
+            it_w.append(iw.mean())
+            it_c.append(ic.mean())
+    assert np.mean(it_w) <= np.mean(it_c)
+    # a reset, and a different batch size, both fall back to a cold solve
+    warm.warm_reset()
+    w = stream[-1]
+    uw, xw, sw, _ = warm.solve(w["x0"], w["u_lin"], w["x_ref"])
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"])
+    assert rel_err(uw, ur).max() <= TOL
+    uw, xw, sw, _ = warm.solve(w["x0"][:100], w["u_lin"][:100], w["x_ref"][:100])
+    assert rel_err(uw, ur[:100]).max() <= TOL
+    warm.close()
+    cold.close()
+
+
+def test_warm_start_gap_rows(oracle, capi):
+    """warm_start with gap rows: W reuse under the GI path."""
+    N, B, T = 20, 256, 4
+    stream = workload.make_stream(B, N, T, seed=12)
+    ranges, *geom = workload.make_scans(B, seed=12)
+    s = capi.Solver(capi.default_config(N, warm_start=1, gap_mode=capi.GAP_ACTIVE))
+    for w in stream:
+        hs = halfspaces_oracle(oracle, w["x0"], ranges, geom)
+        u, x, st, _ = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
+        ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=True)
+        np.testing.assert_array_equal(st, sr)
+        ok = sr == oracle.SOLVED
+        assert rel_err(u[ok], ur[ok]).max() <= TOL
+    s.close()
