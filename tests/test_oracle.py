@@ -288,3 +288,18 @@ def test_oracle_reproduces_golden(oracle, name):
             rc, l1, l2, lo, hi = oracle.find_half_spaces(d["x0"][b].astype(float), d["scan_ranges"][b], *geom)
             assert (lo, hi) == tuple(d["scan_lohi"][b])
             np.testing.assert_array_equal(np.float32([l1, l2]), d["halfspace"][b])
+
+
+def test_osqp_admm_restatement(oracle):
+    """oracle/osqp_admm.c (the CPU baseline, OSQP 0.6 defaults restated) converges to the exact
+    optimum when the tolerances are tightened, and solves every QP at the defaults."""
+    N, B = 20, 64
+    w = workload.make_batch(B, N, seed=41)
+    prm = oracle.params(N)
+    u, x, st = oracle.solve_batch(prm, w["x0"], w["u_lin"], w["x_ref"])
+    ua, sa, ia = oracle.admm_solve_batch(prm, oracle.admm_settings(), w["x0"], w["u_lin"], w["x_ref"])
+    assert (sa == oracle.SOLVED).all() and ia.max() <= 4000
+    tight = oracle.admm_settings(eps_abs=1e-10, eps_rel=1e-10, max_iter=200000)
+    ua, sa, ia = oracle.admm_solve_batch(prm, tight, w["x0"], w["u_lin"], w["x_ref"])
+    assert (sa == oracle.SOLVED).all()
+    np.testing.assert_allclose(ua, u, atol=1e-5)
