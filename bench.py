@@ -33,7 +33,12 @@ CONFIGS = {
                                    "stream (x0 advances 4.5*dt per step, KKT factor reused)"),
     "c5_cold": (4096, 20, False, False, "configs[4] stream solved cold (no warm start), for comparison"),
     "c2_big": (65536, 20, False, False, "throughput: batch=65536 QPs, horizon=20, box constraints"),
+    # global batch, sharded over the ranks (strong scaling): 546 scenarios x 120 candidates + 16
+    "c4": (65536, 40, False, False, "configs[3]: batch=65536 QPs, horizon=40, 6-lane x 20 mini-trajectory "
+                                    "candidate sets (grouped), sharded over the GPUs"),
 }
+STRONG = {"c4"}
+GROUP = 120  # candidates per scenario in c4 (6 lane offsets x 20 steer values)
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
@@ -116,6 +121,49 @@ def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int):
                 exact_oracle_qps=n2 / el2)
 
 
+def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
+    """p50/p99 wall latency (µs) of one QP solve and of one launch of the configured batch."""
+    import torch
+
+    def pct(v):
+        v = np.sort(np.asarray(v) * 1e6)
+        return {"p50_us": float(np.percentile(v, 50)), "p99_us": float(np.percentile(v, 99)),
+                "min_us": float(v[0])}
+
+    one = {k: torch.from_numpy(np.ascontiguousarray(w[k][:1])).to(dev) for k in ("x0", "u_lin", "x_ref")}
+    h1 = None if hs is None else hs[:1].contiguous()
+    uo = torch.empty((1, N, 2), dtype=torch.float32, device=dev)
+    xo = torch.empty((1, N + 1, 3), dtype=torch.float32, device=dev)
+    st = torch.empty((1,), dtype=torch.int32, device=dev)
+    c1 = type(cfg).from_buffer_copy(cfg)
+    c1.warm_start = 0  # a cold solve per call: the latency of one control tick
+    s1 = capi.Solver(c1)
+    dev_t, host_t, batch_t = [], [], []
+    for i in range(reps + 20):
+        t0 = time.perf_counter()
+        s1.solve_dev(one["x0"], one["u_lin"], one["x_ref"], h1, uo, xo, st, stream=stream)
+        stream.synchronize()
+        if i >= 20:
+            dev_t.append(time.perf_counter() - t0)
+    hx = {k: np.ascontiguousarray(w[k][:1]) for k in ("x0", "u_lin", "x_ref")}
+    hh = None if hs is None else hs[:1].cpu().numpy()
+    for i in range(reps + 20):
+        t0 = time.perf_counter()
+        s1.solve(hx["x0"], hx["u_lin"], hx["x_ref"], hh)
+        if i >= 20:
+            host_t.append(time.perf_counter() - t0)
+    s1.close()
+    for i in range(min(reps, 100) + 5):
+        t0 = time.perf_counter()
+        step()
+        stream.synchronize()
+        if i >= 5:
+            batch_t.append(time.perf_counter() - t0)
+    return {"single_qp_device": pct(dev_t), "single_qp_host_pointers": pct(host_t),
+            "batch_launch": pct(batch_t),
+            "note": "wall clock per call incl. launch + stream sync; host-pointer path adds H2D/D2H over PCIe"}
+
+
 def _halfspaces_host(w, B):
     from f110qp import capi, workload
 
@@ -157,8 +205,17 @@ def main():
     Bper, N, gap, warm, desc = CONFIGS[args.config]
     if args.batch:
         Bper = args.batch
+    strong = args.config in STRONG
     stream_cfg = args.config.startswith("c5")
-    if stream_cfg:
+    if strong:
+        # one global batch of grouped candidates; this rank solves its scenario-aligned shard
+        from f110qp import shard
+        total = Bper
+        lo, hi = shard.shard_range(total, world, rank, GROUP)
+        g = workload.make_grouped_batch(-(-total // GROUP), N, seed=4000)
+        w = {k: np.ascontiguousarray(g[k][:total][lo:hi]) for k in ("x0", "u_lin", "x_ref")}
+        Bper = hi - lo
+    elif stream_cfg:
         # one tick of the stream per step, all ticks staged in HBM before timing
         nt = args.warmup + args.steps + 20
         ticks = workload.make_stream(Bper, N, nt, seed=1000 + rank)
@@ -166,7 +223,7 @@ def main():
         UL = torch.from_numpy(np.stack([t["u_lin"] for t in ticks])).to(dev)
         XR = torch.from_numpy(np.stack([t["x_ref"] for t in ticks])).to(dev)
         w = ticks[0]
-    else:
+    elif not strong:
         w = workload.make_batch(Bper, N, seed=1000 + rank)
     x0 = torch.from_numpy(w["x0"]).to(dev)
     ul = torch.from_numpy(w["u_lin"]).to(dev)
@@ -229,7 +286,20 @@ def main():
     torch.cuda.synchronize(dev)
     kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))  # ms per launch
 
-    total_qps = Bper * world * args.steps
+    # per-QP latency: single-QP solves (B = 1) through the device entry point (launch + sync)
+    # and through the host-pointer entry point (H2D + launch + D2H), plus the per-launch
+    # distribution of the configured batch; rank 0 only, outside the timed region
+    latency = None
+    if rank == 0:
+        latency = measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step)
+
+    if strong:
+        tq = torch.tensor([Bper], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(tq)
+        total_qps = int(tq.item()) * args.steps
+    else:
+        total_qps = Bper * world * args.steps
     value = total_qps / el
     ms_per_step = el / args.steps * 1e3
     bpq = bytes_per_qp(N, gap, warm)
@@ -240,7 +310,7 @@ def main():
     traffic = load_traffic(args.config)
 
     out = {
-        "metric": "QP solves/s (horizon=20, nx=3 reference model, nu=2)",
+        "metric": f"QP solves/s (horizon={N}, nx=3 reference model, nu=2)",
         "value": value,
         "unit": "QP solves/s",
         "n_gpus": world,
@@ -248,18 +318,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "fp32 (fp64 refinement)",
         "data": "synthetic (seeded; SURVEY.md 8(d) recipe: simulate_dynamics mini paths)",
         "config": {
             "workload": desc,
             "batch_per_gpu": Bper,
-            "global_batch": Bper * world,
+            "global_batch": total_qps // args.steps,
             "horizon": N,
             "gap_rows": bool(gap),
             "warm_start": bool(warm),
-            "parallelism": f"independent QP shards x{world} (no collective)",
+            "parallelism": f"independent QP shards x{world} (no collective)"
+                           + (f", scenario-aligned ({GROUP}) split of one global batch" if strong else ""),
             "solved_fraction": solved,
             "mean_active_set_iters": float(itn.mean()),
             "max_active_set_iters": int(itn.max()),
@@ -279,6 +350,8 @@ def main():
             "note": "latency-bound (serial active-set chain per wave); neither HBM nor FP32 peak binds",
         },
     }
+    if latency is not None:
+        out["latency"] = latency
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config, N, gap, args.cpu_seconds, args.cpu_threads)

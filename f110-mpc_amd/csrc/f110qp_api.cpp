@@ -83,8 +83,8 @@ void f110qp_default_config(f110qp_config* c, int horizon) {
 
 static int validate_config(const f110qp_config* c) {
   if (!c) return fail(F110QP_ERR_INVALID, "config is NULL");
-  if (c->horizon < 1 || c->horizon > 32)
-    return fail(F110QP_ERR_INVALID, "horizon must be in [1, 32] (one wave holds 2N inputs)");
+  if (c->horizon < 1 || c->horizon > F110QP_MAX_HORIZON)
+    return fail(F110QP_ERR_INVALID, "horizon must be in [1, 48] (one wave holds 2N inputs in <= 2 register rows)");
   if (!(c->dt > 0.f) || !std::isfinite(c->dt)) return fail(F110QP_ERR_INVALID, "dt must be > 0");
   for (int i = 0; i < 3; i++)
     if (!(c->q[i] >= 0.0)) return fail(F110QP_ERR_INVALID, "Q must be >= 0");
@@ -152,11 +152,13 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
   *ws = f110qp::WarmState();
   if (!c->cfg.warm_start) return F110QP_OK;
   const size_t B = (size_t)batch, nu = 2 * (size_t)c->cfg.horizon;
+  const size_t rows = (nu + 63) / 64;  // register rows per lane (act masks: 2 x 64 bits per row)
   hipError_t e;
-  if ((e = c->wW.ensure(B * nu * nu * 4)) || (e = c->wkey.ensure(B * 16)) || (e = c->wact.ensure(B * 16)))
+  if ((e = c->wW.ensure(B * nu * nu * 4)) || (e = c->wkey.ensure(B * 16)) ||
+      (e = c->wact.ensure(B * 16 * rows)))
     return hip_fail(e, "hipMalloc warm-start state");
   if (c->warm_batch != batch) {
-    if ((e = hipMemsetAsync(c->wkey.p, 0, B * 16, s)) || (e = hipMemsetAsync(c->wact.p, 0, B * 16, s)))
+    if ((e = hipMemsetAsync(c->wkey.p, 0, B * 16, s)) || (e = hipMemsetAsync(c->wact.p, 0, B * 16 * rows, s)))
       return hip_fail(e, "hipMemsetAsync warm-start state");
     c->warm_batch = batch;
   }

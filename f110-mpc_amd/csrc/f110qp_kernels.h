@@ -26,7 +26,8 @@ struct KParams {
 // Warm-start state of a context (all null = cold solve). Per QP slot b of the batch:
 //   W[b]   the cached W = H^-1 (2N x 2N, fp32) of the last solve of slot b,
 //   key[b] the float bits of (theta0, v_lin, delta_lin) it was built for + a valid flag,
-//   act[b] the active bounds at the last solution (bit v of act[2b]: lower, act[2b+1]: upper).
+//   act[b] the active bounds at the last solution, per register row r of the lane map
+//          (R = ceil(2N/64) rows): bit lane of act[2(R b + r)] lower, act[2(R b + r) + 1] upper.
 // H depends only on the linearisation point (model.cpp:30-59), so a key hit reuses W exactly.
 struct WarmState {
   float* W = nullptr;

@@ -1,0 +1,1427 @@
+// solve_kernel.h — the MI355X (gfx950) hot path of the f110-mpc control tick (kernel templates;
+// instantiated per (NUM, GAP) in solve_inst.hip, dispatched from f110qp_kernels.hip).
+//
+// One 64-lane wavefront per QP instance (one workgroup = one wave), B instances per launch.
+// Per instance, fused in one launch:
+//   1. Model::Linearize                      (reference src/model.cpp:30-59)      fp64, uniform
+//   2. condensing of the tick's QP           (src/mpc.cpp:208-306)                closed form
+//      The dynamics rows x_{i+1} = A x_i + B u_i + C are eliminated. A = I + E with E^2 = 0
+//      (model.cpp:42-46), so Gamma's entries are affine in the stage distance and every
+//      Hessian entry H = R + Gamma'Q Gamma is an O(1) polynomial sum: each lane builds its
+//      rows of H in registers with no GEMM.
+//   3. W = H^-1 by a symmetric Gauss-Jordan sweep, rows in VGPRs, pivot rows broadcast
+//      by readlane.
+//   4. the QP solve that OSQP does in the reference (src/mpc.cpp:133): a primal-dual active
+//      set warm start (box rows) handed to a dual active-set method (Goldfarb-Idnani,
+//      range-space form) on the condensed problem. The Cholesky factor of S_A = N_A' W N_A
+//      lives in LDS; with gap rows the active normals' W n_j and S_A do too (box rows read
+//      them straight from W). The triangular solves walk the active slots with one lane per
+//      slot and readlane broadcasts. Box rows (mpc.cpp:253,281,290) and follow-the-gap rows
+//      (mpc.cpp:249,271,297-298) are the constraint set.
+//   5. two steps of iterative refinement whose residuals are evaluated in fp64 by an adjoint
+//      (costate) recursion written as wave prefix/suffix scans, then an fp64 feasibility
+//      re-check that re-enters step 4 if needed. Exact optimum to ~1e-9, not OSQP's 1e-3.
+//   6. u* and the state rollout x* (MPC::UpdateSolvedTrajectory, mpc.cpp:145-159).
+// Everything is recentred on (x0, y0): the dynamics and cost are translation invariant in
+// (x, y) (model.cpp:42-55), which keeps fp32 exact to ~1e-6 for |x| ~ 50 m.
+//
+// Lane layout. Decision variable v = 2k + a (stage k, a = 0 speed, 1 steering) lives in
+// lane v mod 64, register row r = v / 64: horizons N <= 32 use one row per lane (R = 1), N <=
+// 48 two (R = 2, BASELINE config C4 is N = 40). Every per-variable quantity is an [R] register
+// array, prefix/suffix scans carry across rows, active slots follow the same map.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "f110qp_kernels.h"
+
+namespace f110qp {
+
+// Diagnostic build only (-DF110QP_STAMPS): per-phase s_memtime deltas of every wave, read back
+// with f110qp_read_stamps(). The shipped library never executes a stamp.
+#ifdef F110QP_STAMPS
+constexpr int kStampSlots = 16;
+__device__ unsigned long long g_stamps[65536 * kStampSlots];  // stamps build: one TU (all instantiations)
+#define STAMP(var) unsigned long long var = __builtin_amdgcn_s_memtime()
+#define STAMP_SET(var) var = __builtin_amdgcn_s_memtime()
+#define STAMP_ACC(acc, since) acc += __builtin_amdgcn_s_memtime() - (since)
+#else
+#define STAMP(var)
+#define STAMP_SET(var)
+#define STAMP_ACC(acc, since)
+#endif
+
+// ------------------------------------------------------------------------------------------
+// wave helpers (64 lanes). Cross-lane traffic uses DPP (row shifts / quad permutes /
+// row broadcasts) and readlane, never LDS: every helper is a handful of VALU instructions.
+// They must be called from wave-uniform control flow (all 64 lanes active): readlane of an
+// EXEC-disabled lane returns a stale register, and DPP treats disabled sources as invalid.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+// DPP controls (gfx9 family encodings)
+constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118;
+constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143;
+constexpr int DPP_QUAD_XOR1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_XOR2 = 0x4E;  // quad_perm [2,3,0,1]
+constexpr int DPP_QUAD_ODD = 0xF5;   // quad_perm [1,1,3,3]: every lane gets lane|1
+constexpr int DPP_ROW_HALF_MIRROR = 0x141, DPP_ROW_MIRROR = 0x140;
+
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ int dpp_i(int v) {  // lanes without a source read 0
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xf, false);
+}
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(dpp_i<CTRL, ROWMASK>(__float_as_int(v)));
+}
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v) {
+  int2 p = *reinterpret_cast<int2*>(&v);
+  p.x = dpp_i<CTRL, ROWMASK>(p.x);
+  p.y = dpp_i<CTRL, ROWMASK>(p.y);
+  return *reinterpret_cast<double*>(&p);
+}
+// full-permutation DPPs (every lane has a source)
+template <int CTRL>
+__device__ __forceinline__ float perm_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int perm_i(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double perm_d(double v) {
+  int2 p = *reinterpret_cast<int2*>(&v);
+  p.x = __builtin_amdgcn_mov_dpp(p.x, CTRL, 0xf, 0xf, false);
+  p.y = __builtin_amdgcn_mov_dpp(p.y, CTRL, 0xf, 0xf, false);
+  return *reinterpret_cast<double*>(&p);
+}
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  int2 p = *reinterpret_cast<int2*>(&v);
+  p.x = __builtin_amdgcn_readlane(p.x, l);
+  p.y = __builtin_amdgcn_readlane(p.y, l);
+  return *reinterpret_cast<double*>(&p);
+}
+
+// row r of a per-lane register array, r wave-uniform at run time
+template <int R, typename T>
+__device__ __forceinline__ T pick(const T (&x)[R], int r) {
+  T v = x[0];
+#pragma unroll
+  for (int i = 1; i < R; i++) v = (r == i) ? x[i] : v;
+  return v;
+}
+// value of slot / variable j (lane j mod 64, row j / 64), j wave-uniform
+template <int R>
+__device__ __forceinline__ float rl_f(const float (&x)[R], int j) {
+  return readlane_f(pick<R>(x, j >> 6), j & 63);
+}
+template <int R>
+__device__ __forceinline__ int rl_i(const int (&x)[R], int j) {
+  return readlane_i(pick<R>(x, j >> 6), j & 63);
+}
+
+// inclusive prefix sum over the 64 lanes (row shifts, then row broadcasts 15 and 31)
+__device__ __forceinline__ float scan_incl(float x) {
+  x += dpp_f<DPP_ROW_SHR1>(x);
+  x += dpp_f<DPP_ROW_SHR2>(x);
+  x += dpp_f<DPP_ROW_SHR4>(x);
+  x += dpp_f<DPP_ROW_SHR8>(x);
+  x += dpp_f<DPP_ROW_BCAST15, 0xa>(x);
+  x += dpp_f<DPP_ROW_BCAST31, 0xc>(x);
+  return x;
+}
+__device__ __forceinline__ double scan_incl(double x) {
+  x += dpp_d<DPP_ROW_SHR1>(x);
+  x += dpp_d<DPP_ROW_SHR2>(x);
+  x += dpp_d<DPP_ROW_SHR4>(x);
+  x += dpp_d<DPP_ROW_SHR8>(x);
+  x += dpp_d<DPP_ROW_BCAST15, 0xa>(x);
+  x += dpp_d<DPP_ROW_BCAST31, 0xc>(x);
+  return x;
+}
+__device__ __forceinline__ float lane63(float v) { return readlane_f(v, 63); }
+__device__ __forceinline__ double lane63(double v) { return readlane_d(v, 63); }
+
+// inclusive prefix over all 64R variables (variable order = row-major over (r, lane))
+template <int R, typename T>
+__device__ __forceinline__ void scan_incl_R(T (&x)[R]) {
+  T carry = T(0);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const T p = scan_incl(x[r]);
+    x[r] = p + carry;
+    if (r + 1 < R) carry += lane63(p);
+  }
+}
+// inclusive suffix over all 64R variables: total - inclusive prefix + own
+template <int R, typename T>
+__device__ __forceinline__ void scan_suffix_incl_R(T (&x)[R]) {
+  T p[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) p[r] = x[r];
+  scan_incl_R<R>(p);
+  const T tot = lane63(p[R - 1]);
+#pragma unroll
+  for (int r = 0; r < R; r++) x[r] = tot - p[r] + x[r];
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+  return lane63(scan_incl(v));
+}
+
+// value of lane|1 (the steering lane of the stage pair)
+__device__ __forceinline__ float odd_lane(float v) { return perm_f<DPP_QUAD_ODD>(v); }
+__device__ __forceinline__ double odd_lane(double v) { return perm_d<DPP_QUAD_ODD>(v); }
+
+// argmin of (val, idx) over the wave, result uniform; ties -> smaller idx
+__device__ __forceinline__ void amin_step(float& v, int& i, float ov, int oi) {
+  const bool take = (ov < v) || (ov == v && oi < i);
+  v = take ? ov : v;
+  i = take ? oi : i;
+}
+__device__ __forceinline__ void wave_argmin(float& val, int& idx) {
+  amin_step(val, idx, perm_f<DPP_QUAD_XOR1>(val), perm_i<DPP_QUAD_XOR1>(idx));
+  amin_step(val, idx, perm_f<DPP_QUAD_XOR2>(val), perm_i<DPP_QUAD_XOR2>(idx));
+  amin_step(val, idx, perm_f<DPP_ROW_HALF_MIRROR>(val), perm_i<DPP_ROW_HALF_MIRROR>(idx));
+  amin_step(val, idx, perm_f<DPP_ROW_MIRROR>(val), perm_i<DPP_ROW_MIRROR>(idx));
+  float v0 = readlane_f(val, 0);
+  int i0 = readlane_i(idx, 0);
+  amin_step(v0, i0, readlane_f(val, 16), readlane_i(idx, 16));
+  amin_step(v0, i0, readlane_f(val, 32), readlane_i(idx, 32));
+  amin_step(v0, i0, readlane_f(val, 48), readlane_i(idx, 48));
+  val = v0;
+  idx = i0;
+}
+
+// ------------------------------------------------------------------------------------------
+// linearised model, fp64 (model.cpp:30-59; L = 0.3302f at :32; dt is the float MPC::dt_)
+// ------------------------------------------------------------------------------------------
+struct Lin {
+  double th0, a02, a12, b00, b10, b20, b21, c0, c1, c2;
+};
+
+__device__ __forceinline__ Lin linearize(double th, double v, double d, float dtf) {
+  const double dt = (double)dtf;
+  const double L = (double)0.3302f;
+  double sn, cs, sd, cd;
+  sincos(th, &sn, &cs);
+  sincos(d, &sd, &cd);
+  const double sec2 = 1.0 / (cd * cd);  // pow(cos(d), -2)
+  Lin M;
+  M.th0 = th;
+  M.a02 = -1 * v * sn * dt;           // :42
+  M.a12 = v * cs * dt;                // :43
+  M.b00 = cs * dt;                    // :48
+  M.b10 = sn * dt;                    // :49
+  M.b20 = (sd / cd) * dt / L;         // :50 tan(d)
+  M.b21 = v * sec2 * dt / L;          // :51
+  M.c0 = v * th * sn * dt;            // :53
+  M.c1 = -1 * v * th * cs * dt;       // :54
+  M.c2 = -1 * d * v * sec2 * dt / L;  // :55
+  return M;
+}
+
+// Forward rollout of u (one value per variable) in fp64. Returns, for each row, the
+// recentred state after the variable's stage k (i = k+1) in both lanes of the stage.
+template <int R>
+__device__ __forceinline__ void rollout_f64(const Lin& M, int lane, const double (&u)[R],
+                                            double (&px)[R], double (&py)[R], double (&th)[R]) {
+  const int a = lane & 1;
+  const double beta = a ? M.b21 : M.b20;
+  double s1[R], s2[R], s3[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int k = 32 * r + (lane >> 1);
+    s1[r] = beta * u[r];
+    s2[r] = (double)k * s1[r];
+    s3[r] = a ? 0.0 : u[r];
+  }
+  scan_incl_R<R>(s1);
+  scan_incl_R<R>(s2);
+  scan_incl_R<R>(s3);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int k = 32 * r + (lane >> 1);
+    const double P1 = odd_lane(s1[r]), P2 = odd_lane(s2[r]), V = odd_lane(s3[r]);
+    const double i = (double)(k + 1);
+    th[r] = M.th0 + i * M.c2 + P1;
+    const double sth = i * M.th0 + M.c2 * (i * (i - 1.0) * 0.5) + (i - 1.0) * P1 - P2;
+    px[r] = i * M.c0 + M.a02 * sth + M.b00 * V;
+    py[r] = i * M.c1 + M.a12 * sth + M.b10 * V;
+  }
+}
+
+// Linear part of the rollout (Gamma w, zero initial state, no affine term), fp32.
+template <int R>
+__device__ __forceinline__ void rollout_lin_f32(const Lin& M, int lane, const float (&w)[R],
+                                                float (&X)[R], float (&Y)[R]) {
+  const int a = lane & 1;
+  const float beta = a ? (float)M.b21 : (float)M.b20;
+  const float a02 = (float)M.a02, a12 = (float)M.a12, b00 = (float)M.b00, b10 = (float)M.b10;
+  float s1[R], s2[R], s3[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int k = 32 * r + (lane >> 1);
+    s1[r] = beta * w[r];
+    s2[r] = (float)k * s1[r];
+    s3[r] = a ? 0.f : w[r];
+  }
+  scan_incl_R<R>(s1);
+  scan_incl_R<R>(s2);
+  scan_incl_R<R>(s3);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int k = 32 * r + (lane >> 1);
+    const float P1 = odd_lane(s1[r]), P2 = odd_lane(s2[r]), V = odd_lane(s3[r]);
+    const float sth = (float)k * P1 - P2;  // (i-1)P1 - P2 with i = k+1
+    X[r] = a02 * sth + b00 * V;
+    Y[r] = a12 * sth + b10 * V;
+  }
+}
+
+// Gradient of the tracking objective (mpc.cpp:208-229 cost) minus the gap-row multiplier
+// terms, at u, by the costate recursion lambda_i = Q(x_i - r_i) - mu_i n_i + A' lambda_{i+1},
+// written as suffix scans. px,py,th are the variable-stage states from rollout_f64.
+template <int R>
+__device__ __forceinline__ void grad_f64(const Lin& M, const KParams& P, int lane, int N,
+                                         const double (&u)[R], const double (&px)[R],
+                                         const double (&py)[R], const double (&th)[R],
+                                         const double (&rx)[R], const double (&ry)[R],
+                                         const double (&rth)[R], const double (&gmx)[R],
+                                         const double (&gmy)[R], double (&g)[R]) {
+  const int a = lane & 1;
+  double ex[R], ey[R], et[R], lx[R], ly[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int k = 32 * r + (lane >> 1);
+    const bool contrib = (a == 1) && (k < N);
+    const double i = (double)(k + 1);
+    ex[r] = contrib ? P.q[0] * (px[r] - rx[r]) - gmx[r] : 0.0;
+    ey[r] = contrib ? P.q[1] * (py[r] - ry[r]) - gmy[r] : 0.0;
+    et[r] = contrib ? P.q[2] * (th[r] - rth[r]) : 0.0;
+    lx[r] = i * ex[r];
+    ly[r] = i * ey[r];
+  }
+  scan_suffix_incl_R<R>(ex);
+  scan_suffix_incl_R<R>(lx);
+  scan_suffix_incl_R<R>(ey);
+  scan_suffix_incl_R<R>(ly);
+  scan_suffix_incl_R<R>(et);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int k = 32 * r + (lane >> 1);
+    const double i = (double)(k + 1);
+    const double lth = et[r] + M.a02 * (lx[r] - i * ex[r]) + M.a12 * (ly[r] - i * ey[r]);
+    const double gv = a ? (P.r[1] * (u[r] - P.udes[1]) + M.b21 * lth)
+                        : (P.r[0] * (u[r] - P.udes[0]) + M.b00 * ex[r] + M.b10 * ey[r] + M.b20 * lth);
+    g[r] = (k < N) ? gv : 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// shared memory of one wave / one QP
+// ------------------------------------------------------------------------------------------
+template <int NUM, bool GAP>
+struct Smem {
+  static constexpr int R = (NUM + 63) / 64;
+  static constexpr int VN = 64 * R;      // per-variable vectors (one entry per lane and row)
+  static constexpr int NST = NUM / 2 + 1;  // stages 0..N
+  alignas(16) float W[NUM][NUM];   // W = H^-1, row-major (symmetric: row p == column p)
+  float L[NUM][NUM + 1];           // Cholesky factor of S_A (lower), slots x slots
+  // gap rows only: V[slot][var] = W n_slot and S_A = N_A' W N_A. With box rows alone both are
+  // signed entries of W (n_j = +-e_var) and are read from W directly.
+  float V[GAP ? NUM : 1][NUM];
+  float S[GAP ? NUM : 1][NUM + 1];
+  float vec[VN];                   // broadcast scratch (one entry per variable)
+  float vec2[VN];
+  float stX[NST], stY[NST];        // per-stage linear rollout (stage 1..N)
+  double rx[VN], ry[VN];           // recentred reference of the variable's stage (fp64: x_ref - x0
+                                   // of two floats is not always a float)
+  float rth[VN];
+  float cmult[3 * VN];             // multiplier per constraint id
+  int ids[VN];                     // PDAS: constraint id of each active slot
+  float pmu[VN];                   // PDAS: multiplier of each variable's active bound
+  double d64[VN];
+  double sx64[NST], sy64[NST];
+  Lin M;                           // linearisation of this QP (uniform)
+};
+
+// constraint ids: id = 3*var + t, t = 0 box lower (n = e_var), 1 box upper (n = -e_var),
+// 2 gap row (stage var/2+1, side var&1)
+__device__ __forceinline__ float box_sign(int id) { return (id - 3 * (id / 3) == 0) ? 1.f : -1.f; }
+
+// l = L^-1 v, one lane per active slot (slot j: lane j mod 64, row j / 64); L read from LDS.
+// A plain q-step loop: the slot count is uniform, each step is mul -> readlane -> fma.
+template <int NUM, bool GAP, int R>
+__device__ __forceinline__ void tri_forward(Smem<NUM, GAP>& sm, int lane, int q,
+                                            const float (&rdiag)[R], const float (&v)[R],
+                                            float (&lv)[R]) {
+  float acc[R];
+  const float* Lrow[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    acc[r] = v[r];
+    lv[r] = 0.f;
+    const int row = 64 * r + lane;
+    Lrow[r] = sm.L[row < NUM ? row : NUM - 1];
+  }
+  const int q0 = q < 64 ? q : 64;
+  for (int kk = 0; kk < q0; kk++) {
+    const float t = acc[0] * rdiag[0];
+    const float lk = readlane_f(t, kk);
+    lv[0] = (lane == kk) ? t : lv[0];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = fmaf(-Lrow[r][kk], lk, acc[r]);
+  }
+  if constexpr (R > 1) {
+    for (int kk = 64; kk < q; kk++) {
+      const float t = acc[1] * rdiag[1];
+      const float lk = readlane_f(t, kk - 64);
+      lv[1] = (lane == kk - 64) ? t : lv[1];
+#pragma unroll
+      for (int r = 1; r < R; r++) acc[r] = fmaf(-Lrow[r][kk], lk, acc[r]);
+    }
+  }
+}
+
+// r = L^-T l (backward substitution, column-oriented)
+template <int NUM, bool GAP, int R>
+__device__ __forceinline__ void tri_backward(Smem<NUM, GAP>& sm, int lane, int q,
+                                             const float (&rdiag)[R], const float (&l)[R],
+                                             float (&out)[R]) {
+  float acc[R];
+  int col[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    acc[r] = l[r];
+    out[r] = 0.f;
+    const int c = 64 * r + lane;
+    col[r] = c < NUM ? c : NUM - 1;
+  }
+  if constexpr (R > 1) {
+    for (int jj = q - 1; jj >= 64; jj--) {
+      const float t = acc[1] * rdiag[1];
+      const float rj = readlane_f(t, jj - 64);
+      out[1] = (lane == jj - 64) ? t : out[1];
+#pragma unroll
+      for (int r = 0; r < R; r++) acc[r] = fmaf(-sm.L[jj][col[r]], rj, acc[r]);
+    }
+  }
+  const int q0 = q < 64 ? q : 64;
+  for (int jj = q0 - 1; jj >= 0; jj--) {
+    const float t = acc[0] * rdiag[0];
+    const float rj = readlane_f(t, jj);
+    out[0] = (lane == jj) ? t : out[0];
+    acc[0] = fmaf(-sm.L[jj][col[0]], rj, acc[0]);
+  }
+}
+
+// S_A[i][c] for slot row i (constraint id sid_i) and uniform slot c
+template <int NUM, bool GAP>
+__device__ __forceinline__ float s_entry(Smem<NUM, GAP>& sm, int row, int sid_i, int sid_c, int c) {
+  if constexpr (GAP) {
+    return sm.S[row][c];
+  } else {
+    const int vi = sid_i / 3, vc = sid_c / 3;
+    return box_sign(sid_i) * box_sign(sid_c) * sm.W[vi][vc];
+  }
+}
+
+// L = chol(S_A) of the q active slots (left-looking, one lane per slot row, L in LDS).
+// Sets this lane's 1/L[j][j] for its slots j < q (other entries keep their value).
+template <int NUM, bool GAP, int R>
+__device__ __forceinline__ void chol_slots(Smem<NUM, GAP>& sm, int lane, int q,
+                                           const int (&slot_id)[R], float (&rd)[R]) {
+  for (int c = 0; c < q; c++) {
+    const int sid_c = GAP ? 0 : rl_i<R>(slot_id, c);
+    float s[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      s[r] = 0.f;
+      const int row = 64 * r + lane;
+      if (row < q && row >= c) {
+        float s0 = s_entry<NUM, GAP>(sm, row, slot_id[r], sid_c, c), s1 = 0.f, s2 = 0.f, s3 = 0.f;
+        int i2 = 0;
+        for (; i2 + 4 <= c; i2 += 4) {  // four independent chains: the LDS reads pipeline
+          s0 = fmaf(-sm.L[row][i2 + 0], sm.L[c][i2 + 0], s0);
+          s1 = fmaf(-sm.L[row][i2 + 1], sm.L[c][i2 + 1], s1);
+          s2 = fmaf(-sm.L[row][i2 + 2], sm.L[c][i2 + 2], s2);
+          s3 = fmaf(-sm.L[row][i2 + 3], sm.L[c][i2 + 3], s3);
+        }
+        for (; i2 < c; i2++) s0 = fmaf(-sm.L[row][i2], sm.L[c][i2], s0);
+        s[r] = (s0 + s1) + (s2 + s3);
+      }
+    }
+    const float dcc = sqrtf(rl_f<R>(s, c));
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int row = 64 * r + lane;
+      if (row < q && row >= c) sm.L[row][c] = (row == c) ? dcc : s[r] / dcc;
+      if (row == c) rd[r] = 1.f / dcc;
+    }
+    wsync();
+  }
+}
+
+// y = W x with x in sm.vec; W symmetric so the lane reads column v (consecutive addresses
+// across lanes, conflict free). Variables >= NUM get 0.
+template <int NUM, bool GAP, int R>
+__device__ __forceinline__ void matvec_W(Smem<NUM, GAP>& sm, int lane, float (&y)[R]) {
+  int c[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int v = 64 * r + lane;
+    c[r] = v < NUM ? v : NUM - 1;
+    y[r] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < NUM; j++) {
+    const float xj = sm.vec[j];
+#pragma unroll
+    for (int r = 0; r < R; r++) y[r] = fmaf(sm.W[j][c[r]], xj, y[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) y[r] = (64 * r + lane < NUM) ? y[r] : 0.f;
+}
+
+// n_j' w for the active slot with id slot_id (w in sm.vec2 by variable, gap rows from the
+// per-stage linear rollout in sm.stX/stY).
+template <int NUM, bool GAP>
+__device__ __forceinline__ float slot_dot(Smem<NUM, GAP>& sm, int slot_id, float ga0, float ga1,
+                                          float gb0, float gb1) {
+  const int owner = slot_id / 3, t = slot_id - 3 * owner;
+  if (t == 0) return sm.vec2[owner];
+  if (t == 1) return -sm.vec2[owner];
+  const int st = (owner >> 1) + 1;
+  return ((owner & 1) ? ga1 : ga0) * sm.stX[st] + ((owner & 1) ? gb1 : gb0) * sm.stY[st];
+}
+
+// column c of V[j] = W n_j for uniform slot j with id sid_j
+template <int NUM, bool GAP>
+__device__ __forceinline__ float vcol(Smem<NUM, GAP>& sm, int j, int sid_j, int c) {
+  if constexpr (GAP) return sm.V[j][c];
+  else return box_sign(sid_j) * sm.W[sid_j / 3][c];
+}
+
+// One pivot of the symmetric sweep operator (Goodnight 1979) on the rows held by this lane:
+//   a_ij -= a_ip a_pj / a_pp ; a_ip /= a_pp ; a_pj /= a_pp ; a_pp = -1/a_pp.
+// The pivot row is broadcast by readlane; the pivot row's own update folds into the common FMA
+// with f = 1 - 1/a_pp. After all pivots the rows hold -H^-1. P is a template constant so every
+// register index is static (no scratch).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int NUM, int R, int P>
+__device__ __forceinline__ void sweep_step(float (&hrow)[R][NUM], int lane) {
+  constexpr int PR = P / 64, PL = P % 64;
+  // pivot row broadcast by readlane (lane PL, static register index) -> SGPR operands
+  float rk[NUM];
+#pragma unroll
+  for (int j = 0; j < NUM; j++) rk[j] = readlane_f(hrow[PR][j], PL);
+  const float inv = __builtin_amdgcn_rcpf(rk[P]);  // 1 ulp; the fp64 refinement absorbs it
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const bool piv = (r == PR) && (lane == PL);
+    const float hp = hrow[r][P];
+    const float f = piv ? (1.f - inv) : hp * inv;
+    const f32x2 nf = {-f, -f};
+#pragma unroll
+    for (int j = 0; j < NUM; j += 2) {  // packed FMA over column pairs (v_pk_fma_f32)
+      const f32x2 rr = {rk[j], rk[j + 1]};
+      f32x2 h = {hrow[r][j], hrow[r][j + 1]};
+      h = __builtin_elementwise_fma(nf, rr, h);
+      hrow[r][j] = h.x;
+      hrow[r][j + 1] = h.y;
+    }
+    hrow[r][P] = piv ? -inv : hp * inv;
+  }
+}
+
+template <int NUM, int R, int P>
+struct Sweep {
+  static __device__ __forceinline__ void run(float (&hrow)[R][NUM], int lane) {
+    sweep_step<NUM, R, P>(hrow, lane);
+    Sweep<NUM, R, P + 1>::run(hrow, lane);
+  }
+};
+template <int NUM, int R>
+struct Sweep<NUM, R, NUM> {
+  static __device__ __forceinline__ void run(float (&)[R][NUM], int) {}
+};
+
+// Build the slots of the bound guess act (0 free, 1 lower, 2 upper) in variable order and
+// factor S_A. Returns the slot count.
+template <int NUM, bool GAP, int R>
+__device__ __forceinline__ int build_box_slots(Smem<NUM, GAP>& sm, int lane, const int (&act)[R],
+                                               int (&slot_id)[R], float (&rd)[R]) {
+  int base = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const unsigned long long mask = __ballot(act[r] != 0);
+    const int myslot = base + __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
+    if (act[r]) sm.ids[myslot] = 3 * (64 * r + lane) + (act[r] == 2 ? 1 : 0);
+    base += __popcll(mask);
+  }
+  wsync();
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int s = 64 * r + lane;
+    slot_id[r] = (s < base) ? sm.ids[s] : -1;
+  }
+  chol_slots<NUM, GAP, R>(sm, lane, base, slot_id, rd);
+  return base;
+}
+
+template <int NUM, bool GAP>
+__global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
+                                                   const float* __restrict__ x0g,
+                                                   const float* __restrict__ ulg,
+                                                   const float* __restrict__ xrg,
+                                                   const float* __restrict__ hsg,
+                                                   float* __restrict__ uout,
+                                                   float* __restrict__ xout,
+                                                   int* __restrict__ status_out,
+                                                   int* __restrict__ iters_out,
+                                                   double* __restrict__ Hdbg,
+                                                   double* __restrict__ gdbg,
+                                                   const WarmState ws) {
+  constexpr int R = (NUM + 63) / 64;
+  __shared__ Smem<NUM, GAP> sm;
+  const int b = blockIdx.x;
+  if (b >= B) return;
+  const int lane = threadIdx.x;
+  const int N = P.N;
+  const int NU = 2 * N;
+  const int a = lane & 1;    // 0 = speed v, 1 = steering
+  int vv[R], kk[R], cl[R];   // variable, its input stage, clamped LDS column
+  bool valid[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    vv[r] = 64 * r + lane;
+    kk[r] = vv[r] >> 1;
+    valid[r] = vv[r] < NU;
+    cl[r] = vv[r] < NUM ? vv[r] : NUM - 1;
+  }
+
+  STAMP(t_start);
+#ifdef F110QP_STAMPS
+  unsigned long long acc_refine = 0, acc_s1 = 0, acc_w = 0, acc_vj = 0, acc_tri = 0, acc_z = 0,
+                     acc_step = 0, acc_upd = 0, acc_pdas = 0;
+#endif
+  // ---- 1. inputs + Model::Linearize ----------------------------------------------------
+  const float fX0 = x0g[3 * b + 0], fY0 = x0g[3 * b + 1], fTH0 = x0g[3 * b + 2];
+  const double X0 = (double)fX0, Y0 = (double)fY0;
+  {
+    const Lin M = linearize((double)fTH0, (double)ulg[2 * b + 0], (double)ulg[2 * b + 1], P.dt);
+    if (lane == 0) sm.M = M;
+    // reference point of the variable's state stage i = k+1 (terminal reuses x_ref[N-1],
+    // mpc.cpp:228), recentred in fp64.
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      double rx = 0.0, ry = 0.0;
+      float rth = 0.f;
+      if (valid[r]) {
+        const int ri = (kk[r] + 1 < N) ? kk[r] + 1 : N - 1;
+        const float* xr = xrg + ((size_t)b * N + ri) * 3;
+        rx = (double)xr[0] - X0;
+        ry = (double)xr[1] - Y0;
+        rth = xr[2];
+      }
+      sm.rx[vv[r]] = rx; sm.ry[vv[r]] = ry; sm.rth[vv[r]] = rth;
+    }
+  }
+  const float umin0 = P.umin[0], umin1 = P.umin[1], umax0 = P.umax[0], umax1 = P.umax[1];
+  float lb[R], ub[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    lb[r] = valid[r] ? (a ? umin1 : umin0) : -3.0e38f;
+    ub[r] = valid[r] ? (a ? umax1 : umax0) : 3.0e38f;
+  }
+
+  // gap rows: a*x + b*y >= -(c+0.5) (constraints.cpp:255-264, mpc.cpp:297-298), recentred
+  float ga0 = 0.f, ga1 = 0.f, gb0 = 0.f, gb1 = 0.f;
+  double gbeta0 = 0.0, gbeta1 = 0.0;
+  bool infeasible0 = false;
+  if (GAP) {
+    const float* h6 = hsg + 6 * b;
+    ga0 = h6[0]; gb0 = h6[1]; ga1 = h6[3]; gb1 = h6[4];
+    gbeta0 = -(double)h6[2] - (double)ga0 * X0 - (double)gb0 * Y0;
+    gbeta1 = -(double)h6[5] - (double)ga1 * X0 - (double)gb1 * Y0;
+    // the stage-0 rows are constant (x0 lies on both lines): infeasible only if violated
+    if (gbeta0 > 1e-9 * (1.0 + fabs((double)h6[2])) || gbeta1 > 1e-9 * (1.0 + fabs((double)h6[5])))
+      infeasible0 = true;
+    if (!(isfinite(gbeta0) && isfinite(gbeta1))) infeasible0 = true;
+  }
+  wsync();
+
+  // warm start: does the cached W of this slot belong to the same linearisation point?
+  const bool warm = ws.W != nullptr && Hdbg == nullptr;
+  bool whit = false, wvalid = false;
+  if (warm) {
+    const unsigned* key = ws.key + 4 * b;
+    wvalid = key[3] == 1u;
+    whit = wvalid && key[0] == __float_as_uint(fTH0) && key[1] == __float_as_uint(ulg[2 * b + 0]) &&
+           key[2] == __float_as_uint(ulg[2 * b + 1]);
+  }
+  STAMP(t_lin);
+  // ---- 2a. gradient at u = 0 (fp64 adjoint) and the free response ------------------------
+  float cgap[R], gnorm = 1.f;
+  {
+    const Lin M = sm.M;
+    double zero[R], px0[R], py0[R], th0s[R], rxd[R], ryd[R], rthd[R], g64[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      zero[r] = 0.0;
+      rxd[r] = sm.rx[vv[r]]; ryd[r] = sm.ry[vv[r]]; rthd[r] = sm.rth[vv[r]];
+      cgap[r] = 0.f;
+    }
+    rollout_f64<R>(M, lane, zero, px0, py0, th0s);
+    // cross-lane helpers run with all 64 lanes active (variables >= 2N contribute zeros)
+    grad_f64<R>(M, P, lane, N, zero, px0, py0, th0s, rxd, ryd, rthd, zero, zero, g64);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const double gv = valid[r] ? g64[r] : 0.0;
+      sm.vec[vv[r]] = (float)gv;
+      if (Hdbg && valid[r]) gdbg[(size_t)b * NU + vv[r]] = gv;
+    }
+    if (GAP) {
+      const double gah = a ? ga1 : ga0, gbh = a ? gb1 : gb0, gbe = a ? gbeta1 : gbeta0;
+#pragma unroll
+      for (int r = 0; r < R; r++) cgap[r] = (float)(gah * px0[r] + gbh * py0[r] - gbe);  // slack = a X + b Y + cgap
+      gnorm = (float)sqrt(gah * gah + gbh * gbh) + 1.f;
+    }
+  }
+
+  STAMP(t_grad);
+  STAMP(t_hess);
+  STAMP(t_inv);
+  if (whit) {
+    // ---- 2b/3 (warm hit): W from the slot cache, no Hessian, no sweep ------------------
+    const float* Wc = ws.W + (size_t)b * NU * NU;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (vv[r] >= NUM) continue;
+#pragma unroll 4
+      for (int j = 0; j < NUM; j++) {
+        float wv = (j == vv[r]) ? 1.f : 0.f;
+        if (j < NU && valid[r]) wv = Wc[(size_t)j * NU + vv[r]];
+        sm.W[j][vv[r]] = wv;
+      }
+    }
+    wsync();
+  } else {
+  // ---- 2b. condensed Hessian rows (closed form, fp32) -------------------------------------
+  // Row v = (k, a), column w = (l, b). For l <= k the stages that see both inputs are
+  // i = k+1..N (T = N-k of them), and Gamma_i[:, w] is affine in the stage distance, so
+  //   H[v][w] = C0_b + C1_b * (k - l)
+  // with four per-row constants (sums of 1, t, t^2 over the T stages). The entries with
+  // l > k are the transpose: every lane publishes its lower rows and reads column v back.
+  float hrow[R][NUM];
+  {
+    const Lin M = sm.M;
+    const float fa02 = (float)M.a02, fa12 = (float)M.a12, fb00 = (float)M.b00;
+    const float fb10 = (float)M.b10, fb20 = (float)M.b20, fb21 = (float)M.b21;
+    const float q0 = (float)P.q[0], q1 = (float)P.q[1], q2 = (float)P.q[2];
+    const float ra = a ? (float)P.r[1] : (float)P.r[0];
+    const float beta_a = a ? fb21 : fb20;
+    const float pxa = a ? 0.f : fb00, pya = a ? 0.f : fb10;  // dk = 0 in this regime
+    const float sxa = fa02 * beta_a, sya = fa12 * beta_a;
+    float C0[R][2], C1[R][2];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const float T = (float)(N - kk[r]);
+      const float S1 = T * (T - 1.f) * 0.5f;
+      const float S2 = (T - 1.f) * T * (2.f * T - 1.f) * (1.f / 6.f);
+      const float Ux = T * pxa + sxa * S1, Vx = pxa * S1 + sxa * S2;
+      const float Uy = T * pya + sya * S1, Vy = pya * S1 + sya * S2;
+#pragma unroll
+      for (int bb = 0; bb < 2; bb++) {
+        const float beta_b = bb ? fb21 : fb20;
+        const float ax_b = bb ? 0.f : fb00, ay_b = bb ? 0.f : fb10;
+        const float sxb = fa02 * beta_b, syb = fa12 * beta_b;
+        C0[r][bb] = q0 * (ax_b * Ux + sxb * Vx) + q1 * (ay_b * Uy + syb * Vy) + q2 * T * beta_a * beta_b;
+        C1[r][bb] = q0 * sxb * Ux + q1 * syb * Uy;
+      }
+      if (vv[r] < NUM) {
+#pragma unroll
+        for (int w = 0; w < NUM; w++) {
+          const int l = w >> 1, bb = w & 1;
+          sm.W[vv[r]][w] = fmaf(C1[r][bb], (float)(kk[r] - l), C0[r][bb]);
+        }
+      }
+    }
+    wsync();
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+#pragma unroll
+      for (int w = 0; w < NUM; w++) {
+        const int l = w >> 1, bb = w & 1;
+        float h = (l <= kk[r]) ? fmaf(C1[r][bb], (float)(kk[r] - l), C0[r][bb]) : sm.W[w][cl[r]];
+        if (w == vv[r]) h += ra;
+        const bool ok = valid[r] && (w < NU);
+        hrow[r][w] = ok ? h : (w == vv[r] ? 1.f : 0.f);
+      }
+    }
+    wsync();
+  }
+  if (Hdbg) {  // debug/parity hook: dump H (g was written above), no solve
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (valid[r]) {
+#pragma unroll
+        for (int w = 0; w < NUM; w++)
+          if (w < NU) Hdbg[((size_t)b * NU + vv[r]) * NU + w] = (double)hrow[r][w];
+      }
+    }
+    return;
+  }
+  STAMP_SET(t_hess);
+  // ---- 3. W = H^-1 : symmetric sweep (Goodnight), rows in registers -----------------------
+  Sweep<NUM, R, 0>::run(hrow, lane);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (vv[r] < NUM) {
+#pragma unroll
+      for (int j = 0; j < NUM; j++) sm.W[vv[r]][j] = -hrow[r][j];  // the sweep leaves -H^-1
+    }
+  }
+  wsync();
+  if (warm) {  // prime the slot cache (coalesced: lane v writes column v of every row)
+    float* Wc = ws.W + (size_t)b * NU * NU;
+    for (int j = 0; j < NU; j++) {
+#pragma unroll
+      for (int r = 0; r < R; r++)
+        if (valid[r]) Wc[(size_t)j * NU + vv[r]] = sm.W[j][cl[r]];
+    }
+    if (lane == 0) {
+      unsigned* key = ws.key + 4 * b;
+      key[0] = __float_as_uint(fTH0);
+      key[1] = __float_as_uint(ulg[2 * b + 0]);
+      key[2] = __float_as_uint(ulg[2 * b + 1]);
+      key[3] = 1u;
+    }
+  }
+  wsync();
+  }  // !whit
+
+  STAMP_SET(t_inv);
+  // ---- 4. active set -----------------------------------------------------------------------
+  // x = -W g  (g in sm.vec)
+  float xv[R];
+  matvec_W<NUM, GAP, R>(sm, lane, xv);
+#pragma unroll
+  for (int r = 0; r < R; r++) xv[r] = valid[r] ? -xv[r] : 0.f;
+  wsync();
+
+  int actf[R];           // bit t set when constraint 3*v+t is active
+  int slot_id[R];        // constraint id of active slot (64r + lane), -1 if none
+  float mult[R];         // its multiplier
+  float rdiag[R];        // 1 / L[slot][slot]
+#pragma unroll
+  for (int r = 0; r < R; r++) { actf[r] = 0; slot_id[r] = -1; mult[r] = 0.f; rdiag[r] = 0.f; }
+  int q = 0;
+  int it = 0;
+  const int max_iter = P.max_iter;
+  int status = infeasible0 ? F110QP_PRIMAL_INFEASIBLE_ID : F110QP_SOLVED_ID;
+  int reentries = 0;
+  double u64[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) u64[r] = 0.0;
+  bool final_ok = false;
+  int forced_p = -1;     // violated row found by the fp64 re-check
+  float forced_sp = 0.f;
+
+  // ---- 4a. box rows only: primal-dual active set warm start (Hintermueller-Ito-Kunisch) ----
+  // Each pass solves the equality QP of the current guess by one Schur solve with S_A =
+  // W[A][A] and re-guesses A from the multipliers and the bounds; on these QPs it reaches
+  // the optimal set in <= 5 passes (one-at-a-time GI needs one pass per active bound). Its
+  // fixed point is a valid GI state (independent normals, positive multipliers), so the GI
+  // loop below only confirms it, and resumes from it if the fp64 re-check finds a violated
+  // row. No convergence within kPdasMaxIter passes -> plain GI from the unconstrained point.
+  if (!GAP && status == F110QP_SOLVED_ID) {
+    STAMP(t_pdas);
+    constexpr int kPdasMaxIter = 10;
+    float uunc[R], u[R], mu[R];
+    int act[R];          // 0 free, 1 at the lower bound, 2 at the upper bound
+    int sid[R];          // slot lanes: constraint id of the slot
+    float rdp[R];        // slot lanes: 1 / L[j][j]
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      uunc[r] = xv[r];
+      u[r] = xv[r];
+      mu[r] = 0.f;
+      sm.vec[vv[r]] = uunc[r];
+      act[r] = 0;
+      sid[r] = -1;
+      rdp[r] = 0.f;
+      if (warm && wvalid && valid[r]) {  // previous tick's active bounds seed the first guess
+        const unsigned long long lo_m = ws.act[2 * (R * b + r)], hi_m = ws.act[2 * (R * b + r) + 1];
+        act[r] = ((lo_m >> lane) & 1ull) ? 1 : (((hi_m >> lane) & 1ull) ? 2 : 0);
+      }
+    }
+    int qn = 0;            // slots of the current guess
+    bool converged = false;
+    bool seeded = false;   // warm guess: build its slots before the first solve
+#pragma unroll
+    for (int r = 0; r < R; r++) seeded = seeded || (__ballot(act[r] != 0) != 0);
+    wsync();
+    for (int pit = 0; pit < kPdasMaxIter; pit++) {
+      if (seeded) {
+        seeded = false;
+        qn = build_box_slots<NUM, GAP, R>(sm, lane, act, sid, rdp);
+      }
+      // solve the equality QP of the current slots: mu = S^-1 (b - N'u_unc), u = u_unc + W N mu
+      float rhs[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        rhs[r] = 0.f;
+        if (64 * r + lane < qn) {
+          const int sv = sid[r] / 3;
+          const float sg = box_sign(sid[r]);
+          const float bj = (sg > 0.f) ? ((sv & 1) ? umin1 : umin0) : -((sv & 1) ? umax1 : umax0);
+          rhs[r] = bj - sg * sm.vec[sv];
+        }
+      }
+      float lvp[R];
+      tri_forward<NUM, GAP, R>(sm, lane, qn, rdp, rhs, lvp);
+      tri_backward<NUM, GAP, R>(sm, lane, qn, rdp, lvp, mu);
+#pragma unroll
+      for (int r = 0; r < R; r++) u[r] = uunc[r];
+      for (int j = 0; j < qn; j++) {
+        const int sj = rl_i<R>(sid, j);
+        const float mj = rl_f<R>(mu, j) * box_sign(sj);
+        const float* wr = sm.W[sj / 3];
+#pragma unroll
+        for (int r = 0; r < R; r++) u[r] = fmaf(mj, wr[cl[r]], u[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < R; r++)
+        if (64 * r + lane < qn) sm.pmu[sid[r] / 3] = mu[r];
+      wsync();
+      int nact[R];
+      unsigned long long changed[R];
+      bool any_changed = false, leaves = false;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const float myu = act[r] ? sm.pmu[vv[r]] : 0.f;
+        const bool nlo = valid[r] && ((act[r] == 1 ? myu : 0.f) + (lb[r] - u[r]) > 0.f);
+        const bool nhi = valid[r] && !nlo && ((act[r] == 2 ? myu : 0.f) + (u[r] - ub[r]) > 0.f);
+        nact[r] = nlo ? 1 : (nhi ? 2 : 0);
+        changed[r] = __ballot(nact[r] != act[r]);
+        any_changed = any_changed || changed[r] != 0;
+        leaves = leaves || (__ballot(act[r] != 0 && nact[r] != act[r]) != 0);
+      }
+      if (!any_changed) { converged = true; it = pit + 1; break; }
+      if (qn == 0 || leaves) {
+        // first guess, or a slot leaves / flips side: build slots and chol(S_A) from scratch
+        qn = build_box_slots<NUM, GAP, R>(sm, lane, nact, sid, rdp);
+      } else {
+        // only additions: append each new bound as a slot with one forward solve
+        // (incremental Cholesky row l = L^-1 S[q][:q], L[q][q] = sqrt(S[q][q] - l'l))
+#pragma unroll
+        for (int r0 = 0; r0 < R; r0++) {
+          unsigned long long addm = changed[r0];
+          while (addm) {
+            const int bit = __builtin_ctzll(addm);
+            addm &= addm - 1;
+            const int v = 64 * r0 + bit;
+            const int na = readlane_i(nact[r0], bit);
+            const int nid = 3 * v + (na == 2 ? 1 : 0);
+            const float sg = (na == 1) ? 1.f : -1.f;
+            float sv[R], lrow[R];
+            float ll = 0.f;
+#pragma unroll
+            for (int r = 0; r < R; r++)
+              sv[r] = (64 * r + lane < qn) ? sg * box_sign(sid[r]) * sm.W[v][sid[r] / 3] : 0.f;
+            tri_forward<NUM, GAP, R>(sm, lane, qn, rdp, sv, lrow);
+#pragma unroll
+            for (int r = 0; r < R; r++) ll += (64 * r + lane < qn) ? lrow[r] * lrow[r] : 0.f;
+            ll = wave_sum(ll);
+            const float dnew = sqrtf(sm.W[v][v] - ll);
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+              const int s = 64 * r + lane;
+              if (s < qn) sm.L[qn][s] = lrow[r];
+              if (s == qn) {
+                sm.L[qn][qn] = dnew;
+                sid[r] = nid;
+                rdp[r] = 1.f / dnew;
+              }
+            }
+            qn++;
+            wsync();
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; r++) act[r] = nact[r];
+    }
+    if (converged) {
+      // hand the active set to the GI state: slots, multipliers, chol(S_A)
+      q = qn;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const bool sl = 64 * r + lane < qn;
+        slot_id[r] = sl ? sid[r] : -1;
+        mult[r] = sl ? fmaxf(mu[r], 0.f) : 0.f;
+        rdiag[r] = sl ? rdp[r] : 0.f;
+        actf[r] = act[r];  // bit0 lower, bit1 upper
+        xv[r] = valid[r] ? u[r] : 0.f;
+      }
+      wsync();
+    }
+    STAMP_ACC(acc_pdas, t_pdas);
+  }
+
+  // ---- 4b. dual active set (Goldfarb-Idnani, range space) ---------------------------------
+  while (status == F110QP_SOLVED_ID && !final_ok) {
+    // ---- step 1: most violated inactive constraint (fp32, scaled) ----
+    STAMP(t_s1);
+    int p;
+    float sp;
+    if (forced_p >= 0) {
+      p = forced_p;
+      sp = forced_sp;
+      forced_p = -1;
+    } else {
+      float X[R], Y[R];
+      if (GAP) rollout_lin_f32<R>(sm.M, lane, xv, X, Y);
+      float best = 0.f;
+      int bid = 0x7fffffff;
+      float sraw = 0.f;  // raw slack of this lane's best candidate
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (!valid[r]) continue;
+        const int v = vv[r];
+        const float s0 = xv[r] - lb[r], s1 = ub[r] - xv[r];
+        const float v0 = s0 / (1.f + fabsf(lb[r])), v1 = s1 / (1.f + fabsf(ub[r]));
+        if (!(actf[r] & 1) && v0 < -1e-6f && v0 < best) { best = v0; bid = 3 * v; sraw = s0; }
+        if (!(actf[r] & 2) && v1 < -1e-6f && v1 < best) { best = v1; bid = 3 * v + 1; sraw = s1; }
+        if (GAP) {
+          const float s2 = (a ? ga1 : ga0) * X[r] + (a ? gb1 : gb0) * Y[r] + cgap[r];
+          const float v2 = s2 / gnorm;
+          if (!(actf[r] & 4) && v2 < -1e-6f && v2 < best) { best = v2; bid = 3 * v + 2; sraw = s2; }
+        }
+      }
+      int bid_w = bid;
+      float best_w = best;
+      wave_argmin(best_w, bid_w);
+      if (bid_w != 0x7fffffff) {
+        p = bid_w;
+        sp = readlane_f(sraw, (bid_w / 3) & 63);
+      } else {
+        // ---- 5. refinement in fp64 + exact feasibility re-check ----
+        STAMP(t_ref0);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          sm.cmult[3 * vv[r]] = 0.f;
+          sm.cmult[3 * vv[r] + 1] = 0.f;
+          sm.cmult[3 * vv[r] + 2] = 0.f;
+        }
+        wsync();
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          if (64 * r + lane < q) sm.cmult[slot_id[r]] = mult[r];
+          u64[r] = valid[r] ? (double)xv[r] : 0.0;
+        }
+        const Lin M = sm.M;
+        double rxd[R], ryd[R], rthd[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) { rxd[r] = sm.rx[vv[r]]; ryd[r] = sm.ry[vv[r]]; rthd[r] = sm.rth[vv[r]]; }
+        double px[R], py[R], th[R];
+        for (int rs = 0; rs < 2; rs++) {
+          wsync();
+          rollout_f64<R>(M, lane, u64, px, py, th);
+          double gmx[R], gmy[R];  // gap multipliers of the variable's stage (sides 0,1)
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            gmx[r] = 0.0; gmy[r] = 0.0;
+            if (GAP) {
+              const double m0 = (double)sm.cmult[3 * (vv[r] & ~1) + 2];
+              const double m1 = (double)sm.cmult[3 * (vv[r] | 1) + 2];
+              gmx[r] = m0 * ga0 + m1 * ga1;
+              gmy[r] = m0 * gb0 + m1 * gb1;
+            }
+          }
+          double r1[R];
+          grad_f64<R>(M, P, lane, N, u64, px, py, th, rxd, ryd, rthd, gmx, gmy, r1);
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            r1[r] = valid[r] ? r1[r] : 0.0;
+            if (valid[r]) r1[r] += -(double)sm.cmult[3 * vv[r]] + (double)sm.cmult[3 * vv[r] + 1];
+            sm.d64[vv[r]] = u64[r];
+            if (GAP && a == 1 && kk[r] < N) { sm.sx64[kk[r] + 1] = px[r]; sm.sy64[kk[r] + 1] = py[r]; }
+            sm.vec[vv[r]] = (float)r1[r];
+          }
+          wsync();
+          // r2_j = n_j'u - b_j on the active rows (fp64)
+          float r2[R];
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            r2[r] = 0.f;
+            if (64 * r + lane < q) {
+              const int owner = slot_id[r] / 3, t = slot_id[r] - 3 * owner;
+              if (t == 0) r2[r] = (float)(sm.d64[owner] - (double)((owner & 1) ? umin1 : umin0));
+              else if (t == 1) r2[r] = (float)((double)((owner & 1) ? umax1 : umax0) - sm.d64[owner]);
+              else {
+                const int st = (owner >> 1) + 1;
+                r2[r] = (owner & 1) ? (float)((double)ga1 * sm.sx64[st] + (double)gb1 * sm.sy64[st] - gbeta1)
+                                    : (float)((double)ga0 * sm.sx64[st] + (double)gb0 * sm.sy64[st] - gbeta0);
+              }
+            }
+          }
+          // w1 = W r1 ; v1_j = n_j' w1
+          float w1[R];
+          matvec_W<NUM, GAP, R>(sm, lane, w1);
+#pragma unroll
+          for (int r = 0; r < R; r++) sm.vec2[vv[r]] = w1[r];
+          if (GAP) {
+            float X1[R], Y1[R], w1v[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) w1v[r] = valid[r] ? w1[r] : 0.f;
+            rollout_lin_f32<R>(M, lane, w1v, X1, Y1);
+#pragma unroll
+            for (int r = 0; r < R; r++)
+              if (a == 1 && kk[r] < N) { sm.stX[kk[r] + 1] = X1[r]; sm.stY[kk[r] + 1] = Y1[r]; }
+          }
+          wsync();
+          float rhs[R], lv[R], du[R];
+#pragma unroll
+          for (int r = 0; r < R; r++)
+            rhs[r] = (64 * r + lane < q) ? slot_dot<NUM, GAP>(sm, slot_id[r], ga0, ga1, gb0, gb1) - r2[r] : 0.f;
+          // du = S^-1 rhs ; dx = -w1 + sum_j du_j V[j]
+          tri_forward<NUM, GAP, R>(sm, lane, q, rdiag, rhs, lv);
+          tri_backward<NUM, GAP, R>(sm, lane, q, rdiag, lv, du);
+          float dx[R];
+#pragma unroll
+          for (int r = 0; r < R; r++) dx[r] = -w1[r];
+          for (int j = 0; j < q; j++) {
+            const float duj = rl_f<R>(du, j);
+            const int sj = GAP ? 0 : rl_i<R>(slot_id, j);
+#pragma unroll
+            for (int r = 0; r < R; r++) dx[r] = fmaf(duj, vcol<NUM, GAP>(sm, j, sj, cl[r]), dx[r]);
+          }
+          float adx = 0.f;
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            if (valid[r]) u64[r] += (double)dx[r];
+            mult[r] += du[r];
+            adx = fmaxf(adx, valid[r] ? fabsf(dx[r]) : 0.f);
+          }
+          wsync();
+#pragma unroll
+          for (int r = 0; r < R; r++)
+            if (64 * r + lane < q) sm.cmult[slot_id[r]] = mult[r];
+          // a second step only if the first correction was not already at fp32 noise level
+          int dummy = 0;
+          adx = -adx;
+          wave_argmin(adx, dummy);  // -max |dx|
+          if (-adx <= 1e-5f) break;
+        }
+        wsync();
+        // fp64 feasibility check of every inactive row at the refined point
+        rollout_f64<R>(M, lane, u64, px, py, th);
+        float best64 = 0.f, sp64 = 0.f;
+        int bid64 = 0x7fffffff;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          if (!valid[r]) continue;
+          const int v = vv[r];
+          const double s0 = u64[r] - (double)lb[r], s1 = (double)ub[r] - u64[r];
+          const float v0 = (float)(s0 / (1.0 + fabs((double)lb[r])));
+          const float v1 = (float)(s1 / (1.0 + fabs((double)ub[r])));
+          if (!(actf[r] & 1) && v0 < -1e-9f && v0 < best64) { best64 = v0; bid64 = 3 * v; sp64 = (float)s0; }
+          if (!(actf[r] & 2) && v1 < -1e-9f && v1 < best64) { best64 = v1; bid64 = 3 * v + 1; sp64 = (float)s1; }
+          if (GAP) {
+            const double s2 = a ? ((double)ga1 * px[r] + (double)gb1 * py[r] - gbeta1)
+                                : ((double)ga0 * px[r] + (double)gb0 * py[r] - gbeta0);
+            const float v2 = (float)(s2 / (double)gnorm);
+            if (!(actf[r] & 4) && v2 < -1e-9f && v2 < best64) { best64 = v2; bid64 = 3 * v + 2; sp64 = (float)s2; }
+          }
+        }
+        wave_argmin(best64, bid64);
+        STAMP_ACC(acc_refine, t_ref0);
+        if (bid64 == 0x7fffffff || reentries >= 4) {
+          final_ok = true;
+          break;
+        }
+        reentries++;
+        forced_p = bid64;
+        forced_sp = readlane_f(sp64, (bid64 / 3) & 63);
+#pragma unroll
+        for (int r = 0; r < R; r++) xv[r] = valid[r] ? (float)u64[r] : 0.f;
+        continue;
+      }
+    }
+
+    STAMP_ACC(acc_s1, t_s1);
+    const int pown = p / 3, pt = p - 3 * pown;
+    float uplus_new = 0.f;  // multiplier of the candidate p
+    // ---- step 2: add p (possibly after drops) ----
+    for (;;) {
+      STAMP(t_a);
+      if (++it > max_iter) { status = F110QP_MAX_ITER_ID; break; }
+      // w = W n_p ; nw = n_p' W n_p
+      float w[R], nw;
+      if (pt < 2) {
+        const float sg = (pt == 0) ? 1.f : -1.f;
+#pragma unroll
+        for (int r = 0; r < R; r++) w[r] = (vv[r] < NUM) ? sg * sm.W[pown][vv[r]] : 0.f;
+        nw = sm.W[pown][pown];
+      } else {
+        const int ip = (pown >> 1) + 1, h = pown & 1;
+        const float ah = h ? ga1 : ga0, bh = h ? gb1 : gb0;
+        const Lin& M = sm.M;
+        float np[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          np[r] = 0.f;
+          if (valid[r] && kk[r] < ip) {
+            const float d = (float)(ip - 1 - kk[r]);
+            const float fa02 = (float)M.a02, fa12 = (float)M.a12;
+            if (a == 0) np[r] = ah * ((float)M.b00 + fa02 * (float)M.b20 * d) + bh * ((float)M.b10 + fa12 * (float)M.b20 * d);
+            else np[r] = (ah * fa02 + bh * fa12) * (float)M.b21 * d;
+          }
+          sm.vec[vv[r]] = np[r];
+        }
+        wsync();
+        matvec_W<NUM, GAP, R>(sm, lane, w);
+        float s = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; r++) s += np[r] * w[r];
+        nw = wave_sum(s);
+      }
+      STAMP_ACC(acc_w, t_a);
+      STAMP(t_b);
+      // v_j = n_j' w for the active slots
+#pragma unroll
+      for (int r = 0; r < R; r++) sm.vec2[vv[r]] = w[r];
+      if (GAP) {
+        float Xw[R], Yw[R], wv[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) wv[r] = valid[r] ? w[r] : 0.f;
+        rollout_lin_f32<R>(sm.M, lane, wv, Xw, Yw);
+#pragma unroll
+        for (int r = 0; r < R; r++)
+          if (a == 1 && kk[r] < N) { sm.stX[kk[r] + 1] = Xw[r]; sm.stY[kk[r] + 1] = Yw[r]; }
+      }
+      wsync();
+      float vj[R];
+#pragma unroll
+      for (int r = 0; r < R; r++)
+        vj[r] = (64 * r + lane < q) ? slot_dot<NUM, GAP>(sm, slot_id[r], ga0, ga1, gb0, gb1) : 0.f;
+      STAMP_ACC(acc_vj, t_b);
+      STAMP(t_c);
+      // l = L^-1 v ; r = L^-T l  (r = S_A^-1 N_A' W n_p : dual step direction)
+      float lv[R], rr[R];
+      tri_forward<NUM, GAP, R>(sm, lane, q, rdiag, vj, lv);
+      float lls = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; r++) lls += (64 * r + lane < q) ? lv[r] * lv[r] : 0.f;
+      const float ll = wave_sum(lls);
+      tri_backward<NUM, GAP, R>(sm, lane, q, rdiag, lv, rr);
+      STAMP_ACC(acc_tri, t_c);
+      STAMP(t_d);
+      // z = w - sum_j r_j V[j]  (primal step direction)
+      float z[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) z[r] = w[r];
+      for (int j = 0; j < q; j++) {
+        const float rj = rl_f<R>(rr, j);
+        const int sj = GAP ? 0 : rl_i<R>(slot_id, j);
+#pragma unroll
+        for (int r = 0; r < R; r++) z[r] = fmaf(-rj, vcol<NUM, GAP>(sm, j, sj, cl[r]), z[r]);
+      }
+      const float pivv = nw - ll;  // = z' n_p, the new Schur pivot
+      STAMP_ACC(acc_z, t_d);
+      STAMP(t_e);
+      // partial step t1 (blocking multiplier k1)
+      float t1 = 3.0e38f;
+      int k1 = 0x7fffffff;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const int s = 64 * r + lane;
+        if (s < q && rr[r] > 0.f) {
+          const float tr = mult[r] / rr[r];
+          if (tr < t1) { t1 = tr; k1 = s; }
+        }
+      }
+      wave_argmin(t1, k1);
+      const bool dep = !(pivv > 1e-5f * nw);  // n_p (numerically) in span of the active set
+      const float t2 = dep ? 3.0e38f : -sp / pivv;
+      const float t = fminf(t1, t2);
+      if (t >= 3.0e38f) { status = F110QP_PRIMAL_INFEASIBLE_ID; break; }
+#pragma unroll
+      for (int r = 0; r < R; r++)
+        if (64 * r + lane < q) mult[r] -= t * rr[r];
+      uplus_new += t;
+      bool add = false;
+      if (!dep) {
+#pragma unroll
+        for (int r = 0; r < R; r++)
+          if (valid[r]) xv[r] = fmaf(t, z[r], xv[r]);
+        sp = fmaf(t, pivv, sp);
+        add = (t2 <= t1);
+      }
+      wsync();
+      STAMP_ACC(acc_step, t_e);
+      STAMP(t_f);
+      if (add) {
+        if (q >= NUM) { status = F110QP_MAX_ITER_ID; break; }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const int s = 64 * r + lane;
+          if (GAP) {
+            if (vv[r] < NUM) sm.V[q][vv[r]] = w[r];
+            if (s < q) {
+              sm.S[q][s] = vj[r];
+              sm.S[s][q] = vj[r];
+            }
+          }
+          if (s < q) sm.L[q][s] = lv[r];
+          if (s == q) {
+            slot_id[r] = p;
+            mult[r] = uplus_new;
+            rdiag[r] = 1.f / sqrtf(pivv);
+          }
+          if (vv[r] == pown) actf[r] |= (1 << pt);
+        }
+        if (lane == 0) {
+          if (GAP) sm.S[q][q] = nw;
+          sm.L[q][q] = sqrtf(pivv);
+        }
+        q++;
+        wsync();
+        STAMP_ACC(acc_upd, t_f);
+        break;
+      }
+      // drop slot k1, then retry p
+      {
+        const int kd = k1;
+        const int did = rl_i<R>(slot_id, kd);
+        const int down = did / 3;
+#pragma unroll
+        for (int r = 0; r < R; r++)
+          if (vv[r] == down) actf[r] &= ~(1 << (did - 3 * down));
+        // slots kd+1..q-1 move down by one (lane shift, carrying across register rows)
+        int sid_n[R];
+        float mul_n[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          sid_n[r] = __shfl_down(slot_id[r], 1, 64);
+          mul_n[r] = __shfl_down(mult[r], 1, 64);
+          if (r + 1 < R) {
+            const int s_next = readlane_i(slot_id[r + 1 < R ? r + 1 : r], 0);
+            const float m_next = readlane_f(mult[r + 1 < R ? r + 1 : r], 0);
+            if (lane == 63) { sid_n[r] = s_next; mul_n[r] = m_next; }
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const int s = 64 * r + lane;
+          if (s >= kd && s < q - 1) { slot_id[r] = sid_n[r]; mult[r] = mul_n[r]; }
+          if (s == q - 1) { slot_id[r] = -1; mult[r] = 0.f; }
+        }
+        if (GAP) {
+          // remove slot kd from V (rows) and S (row and column): every lane moves only its own
+          // columns (V, S rows) or its own rows (S columns), so there is no cross-lane hazard
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            if (vv[r] < NUM) {
+              for (int j = kd; j < q - 1; j++) {
+                sm.V[j][vv[r]] = sm.V[j + 1][vv[r]];
+                sm.S[j][vv[r]] = sm.S[j + 1][vv[r]];
+              }
+            }
+          }
+          wsync();
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            const int s = 64 * r + lane;
+            if (s < q - 1)
+              for (int i2 = kd; i2 < q - 1; i2++) sm.S[s][i2] = sm.S[s][i2 + 1];
+          }
+        }
+        q--;
+        wsync();
+        chol_slots<NUM, GAP, R>(sm, lane, q, slot_id, rdiag);
+      }
+    }
+  }
+
+  STAMP(t_gi);
+  // ---- 6. outputs ---------------------------------------------------------------------------
+  if (status == F110QP_SOLVED_ID && !final_ok) status = F110QP_MAX_ITER_ID;
+  const bool ok = (status == F110QP_SOLVED_ID);
+  {
+    double uo[R], px[R], py[R], th[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) uo[r] = (ok && valid[r]) ? u64[r] : 0.0;
+    rollout_f64<R>(sm.M, lane, uo, px, py, th);
+    const float nanv = __int_as_float(0x7fc00000);
+    float* xo = xout + (size_t)b * 3 * (N + 1);
+    if (lane == 0) {
+      xo[0] = ok ? fX0 : nanv;
+      xo[1] = ok ? fY0 : nanv;
+      xo[2] = ok ? fTH0 : nanv;
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (valid[r]) uout[(size_t)b * NU + vv[r]] = ok ? (float)u64[r] : nanv;
+      if (valid[r] && a == 1) {
+        xo[3 * (kk[r] + 1) + 0] = ok ? (float)(px[r] + X0) : nanv;
+        xo[3 * (kk[r] + 1) + 1] = ok ? (float)(py[r] + Y0) : nanv;
+        xo[3 * (kk[r] + 1) + 2] = ok ? (float)th[r] : nanv;
+      }
+    }
+  }
+  if (lane == 0) {
+    status_out[b] = status;
+    if (iters_out) iters_out[b] = it;
+  }
+  if (warm) {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const unsigned long long lo_m = __ballot(ok && valid[r] && (actf[r] & 1));
+      const unsigned long long hi_m = __ballot(ok && valid[r] && (actf[r] & 2));
+      if (lane == 0) {
+        ws.act[2 * (R * b + r)] = lo_m;
+        ws.act[2 * (R * b + r) + 1] = hi_m;
+      }
+    }
+  }
+#ifdef F110QP_STAMPS
+  STAMP(t_end);
+  if (lane == 0 && b < 65536) {
+    unsigned long long* o = g_stamps + (size_t)b * kStampSlots;
+    o[0] = t_lin - t_start; o[1] = t_grad - t_lin; o[2] = t_hess - t_grad; o[3] = t_inv - t_hess;
+    o[4] = t_gi - t_inv - acc_refine; o[5] = acc_refine; o[6] = t_end - t_gi; o[7] = t_end - t_start;
+    o[8] = acc_s1; o[9] = acc_pdas; o[10] = acc_vj; o[11] = acc_tri; o[12] = acc_z; o[13] = acc_step;
+    o[14] = acc_upd; o[15] = it;
+    (void)acc_w;
+  }
+#endif
+}
+
+// ------------------------------------------------------------------------------------------
+// launch of one instantiation
+// ------------------------------------------------------------------------------------------
+template <int NUM, bool GAP>
+hipError_t launch_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
+                    const float* hs, float* uo, float* xo, int* st, int* its, double* Hd,
+                    double* gd, const WarmState& ws, hipStream_t s) {
+  hipLaunchKernelGGL((solve_kernel<NUM, GAP>), dim3(B), dim3(64), 0, s, P, B, x0, ul, xr, hs, uo,
+                     xo, st, its, Hd, gd, ws);
+  return hipGetLastError();
+}
+
+}  // namespace f110qp

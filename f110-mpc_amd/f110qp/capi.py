@@ -25,7 +25,7 @@ PRIMAL_INFEASIBLE = -3
 NUMERICAL = -10
 GAP_INACTIVE = 0
 GAP_ACTIVE = 1
-MAX_HORIZON = 64
+MAX_HORIZON = 48
 
 # every symbol include/f110qp.h declares
 EXPORTED = (

@@ -58,12 +58,12 @@ extern "C" {
 #define F110QP_GAP_INACTIVE 0     /* as shipped: gap rows bounded by +-OsqpEigen::INFTY */
 #define F110QP_GAP_ACTIVE 1       /* a*x+b*y >= -(c+0.5) on stages 1..N (mpc.cpp:297-298) */
 
-#define F110QP_MAX_HORIZON 64
+#define F110QP_MAX_HORIZON 48  /* 2N <= 96 decision variables: two register rows per lane */
 
 typedef struct f110qp_ctx f110qp_ctx;
 
 typedef struct {
-  int horizon;      /* N; params.yaml:12 ("/horizon"), 1..F110QP_MAX_HORIZON          */
+  int horizon;      /* N; params.yaml:12 ("/horizon"), 1..F110QP_MAX_HORIZON (48)     */
   float dt;         /* params.yaml:13, held as float MPC::dt_ (include/f110-mpc/mpc.h:46) */
   double q[3];      /* diag Q: q0,q1,q2 (params.yaml:1-3; mpc.cpp:20-24)                 */
   double r[2];      /* diag R: r0,r1 (params.yaml:5-6)                                    */

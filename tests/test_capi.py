@@ -43,7 +43,7 @@ def test_version_and_defaults(capi):
 
 @pytest.mark.parametrize("over,msg", [
     (dict(horizon=0), "horizon"),
-    (dict(horizon=33), "horizon"),
+    (dict(horizon=49), "horizon"),
     (dict(r=[0.0, 5.0]), "R must be > 0"),
     (dict(q=[-1.0, 10.0, 0.0]), "Q must be"),
     (dict(u_min=[5.0, -0.43]), "u_min > u_max"),

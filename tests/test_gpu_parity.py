@@ -82,13 +82,13 @@ def test_c3_full_batch_gap_rows(oracle, capi):
     assert (st == capi.SOLVED).mean() > 0.99
 
 
-@pytest.mark.parametrize("N", [1, 2, 3, 7, 10, 16, 17, 24, 25, 30, 32])
+@pytest.mark.parametrize("N", [1, 2, 3, 7, 10, 16, 17, 24, 25, 30, 32, 33, 36, 40, 41, 47, 48])
 def test_horizons(oracle, capi, N):
     w = workload.make_batch(200, N, seed=300 + N, lateral=0.6)
     check(oracle, capi, N, w)
 
 
-@pytest.mark.parametrize("N", [5, 12, 20, 32])
+@pytest.mark.parametrize("N", [5, 12, 20, 32, 40, 48])
 def test_horizons_gap(oracle, capi, N):
     B = 300
     w = workload.make_batch(B, N, seed=400 + N)
@@ -96,11 +96,12 @@ def test_horizons_gap(oracle, capi, N):
     check(oracle, capi, N, w, halfspaces_oracle(oracle, w["x0"], ranges, geom), gap=True)
 
 
-def test_true_heading_and_hard_references(oracle, capi):
+@pytest.mark.parametrize("N", [20, 40])
+def test_true_heading_and_hard_references(oracle, capi, N):
     """x_ref with the true heading, large lateral offsets and steer beyond the +-0.43 box:
     many active rows (both box faces)."""
-    w = workload.make_batch(1024, 20, seed=77, heading="true", lateral=2.0, steer_range=1.2)
-    u, x, st, it = check(oracle, capi, 20, w)
+    w = workload.make_batch(1024, N, seed=77, heading="true", lateral=2.0, steer_range=1.2)
+    u, x, st, it = check(oracle, capi, N, w)
     lo = np.float32([3.0, -0.43])
     hi = np.float32([4.5, 0.43])
     n_active = ((np.abs(u - lo) < 1e-6) | (np.abs(u - hi) < 1e-6)).sum(axis=(1, 2))
@@ -207,7 +208,7 @@ def test_condensed_hessian_and_gradient(oracle, capi, cuda):
     Gamma'Q Gamma (mpc.cpp:208-229 eliminated through the dynamics rows)."""
     import torch
 
-    for N in (1, 7, 20, 32):
+    for N in (1, 7, 20, 32, 40, 48):
         B = 16
         w = workload.make_batch(B, N, seed=600 + N)
         s = capi.Solver(capi.default_config(N))
@@ -316,3 +317,34 @@ def test_warm_start_gap_rows(oracle, capi):
         ok = sr == oracle.SOLVED
         assert rel_err(u[ok], ur[ok]).max() <= TOL
     s.close()
+
+
+def test_c4_grouped_candidates_horizon40(oracle, capi):
+    """BASELINE configs[3] per GPU: 8,192 horizon-40 QPs (a 1/8 shard of 65,536 = 546
+    scenarios x 120 candidates + remainder), two register rows per lane. All solved, parity on
+    a strided sample plus every candidate of two whole scenarios."""
+    N = 40
+    w = workload.make_grouped_batch(69, N, seed=4040)
+    B = 8192
+    w = {k: (v[:B] if isinstance(v, np.ndarray) else v) for k, v in w.items()}
+    s = capi.Solver(capi.default_config(N))
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    assert (st == capi.SOLVED).all()
+    idx = np.concatenate([np.arange(0, B, 37), np.arange(120, 360)])
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
+    assert (sr == oracle.SOLVED).all()
+    assert rel_err(u[idx], ur).max() <= TOL and rel_err(x[idx], xr).max() <= TOL
+
+
+def test_warm_started_stream_horizon40(oracle, capi):
+    """warm_start at N = 40: the act masks of both register rows carry across ticks."""
+    N, B, T = 40, 256, 4
+    stream = workload.make_stream(B, N, T, seed=21, heading_change_every=2)
+    warm = capi.Solver(capi.default_config(N, warm_start=1))
+    for w in stream:
+        uw, xw, sw, iw = warm.solve(w["x0"], w["u_lin"], w["x_ref"])
+        ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"])
+        np.testing.assert_array_equal(sw, sr)
+        assert rel_err(uw, ur).max() <= TOL and rel_err(xw, xr).max() <= TOL
+    warm.close()
