@@ -186,6 +186,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--backend", default="auto", choices=["auto", "wave", "lane"],
+                    help="solver back end (auto: lane-per-QP for box-only batches >= 2048)")
     args = ap.parse_args()
 
     import torch
@@ -237,15 +239,17 @@ def main():
     xo = torch.empty((Bper, N + 1, 3), dtype=torch.float32, device=dev)
     st = torch.empty((Bper,), dtype=torch.int32, device=dev)
     it = torch.empty((Bper,), dtype=torch.int32, device=dev)
+    backend = {"auto": capi.BACKEND_AUTO, "wave": capi.BACKEND_WAVE, "lane": capi.BACKEND_LANE}[args.backend]
     cfg = capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, device=dev.index,
-                              warm_start=int(warm))
+                              warm_start=int(warm), backend=backend)
+    lane = (not gap) and (backend == capi.BACKEND_LANE or (backend == capi.BACKEND_AUTO and Bper >= capi.LANE_MIN_BATCH))
     solver = capi.Solver(cfg)
     stream = torch.cuda.current_stream(dev)
     tick = [0]
 
     def step():
         if stream_cfg:
-            t = tick[0]
+            t = tick[0] % X0.shape[0]  # the latency probe after the timed region wraps around
             tick[0] += 1
             solver.solve_dev(X0[t], UL[t], XR[t], hs, uo, xo, st, it, stream=stream)
         else:
@@ -329,6 +333,7 @@ def main():
             "horizon": N,
             "gap_rows": bool(gap),
             "warm_start": bool(warm),
+            "backend": "lane-per-QP (Riccati/PDAS fp64)" if lane else "wave-per-QP (condensed, PDAS/GI)",
             "parallelism": f"independent QP shards x{world} (no collective)"
                            + (f", scenario-aligned ({GROUP}) split of one global batch" if strong else ""),
             "solved_fraction": solved,
@@ -342,7 +347,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "f110qp::solve_kernel",
+            "kernel": "f110qp::lane_kernel (+ solve_kernel hand-over launch)" if lane else "f110qp::solve_kernel",
             "kernel_ms_per_launch": kms,
             "algorithmic_bytes_per_qp": bpq,
             "fp32_compute": {"achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -56,6 +57,10 @@ struct f110qp_ctx {
   DevBuf x0, ul, xr, hs, uo, xo, st, it;
   DevBuf wW, wkey, wact;  // warm-start slot state (config.warm_start)
   int warm_batch = 0;     // batch size the warm state was laid out for
+  DevBuf lscr, lfail, lcnt;  // lane back end: Riccati scratch, hand-over list, 2 counters
+  int lane_parity = 0;       // which of the two counters this call appends to
+  int lane_kmax = 16;        // PDAS passes of the lane back end before the wave kernel takes over
+  int lane_mode = 0;         // lane scratch placement (LaneWork::mode)
   hipStream_t stream = nullptr;
 };
 
@@ -79,6 +84,7 @@ void f110qp_default_config(f110qp_config* c, int horizon) {
   c->max_iter = 0;
   c->device = 0;
   c->warm_start = 0;
+  c->backend = F110QP_BACKEND_AUTO;
 }
 
 static int validate_config(const f110qp_config* c) {
@@ -96,6 +102,8 @@ static int validate_config(const f110qp_config* c) {
     return fail(F110QP_ERR_INVALID, "gap_mode must be F110QP_GAP_INACTIVE or F110QP_GAP_ACTIVE");
   if (c->max_iter < 0) return fail(F110QP_ERR_INVALID, "max_iter must be >= 0");
   if (c->warm_start != 0 && c->warm_start != 1) return fail(F110QP_ERR_INVALID, "warm_start must be 0 or 1");
+  if (c->backend < F110QP_BACKEND_AUTO || c->backend > F110QP_BACKEND_LANE)
+    return fail(F110QP_ERR_INVALID, "backend must be F110QP_BACKEND_AUTO, _WAVE or _LANE");
   return F110QP_OK;
 }
 
@@ -117,6 +125,16 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     k.umin[i] = cfg->u_min[i];
     k.umax[i] = cfg->u_max[i];
   }
+  // test hook: F110QP_LANE_KMAX forces early hand-over from the lane to the wave back end
+  if (const char* ek = std::getenv("F110QP_LANE_KMAX")) {
+    const int v = std::atoi(ek);
+    if (v >= 1 && v <= 64) c->lane_kmax = v;
+  }
+  // test/bench hook: F110QP_LANE_MODE = 1 LDS fp64, 2 LDS fp32, 3 HBM fp64 scratch
+  if (const char* em = std::getenv("F110QP_LANE_MODE")) {
+    const int v = std::atoi(em);
+    if (v >= 0 && v <= 3) c->lane_mode = v;
+  }
   const int nu = 2 * cfg->horizon;
   k.max_iter = cfg->max_iter > 0 ? cfg->max_iter : 8 * (nu + (cfg->gap_mode ? nu : 0)) + 16;
   *out = c;
@@ -128,6 +146,7 @@ void f110qp_destroy(f110qp_ctx* c) {
   c->x0.release(); c->ul.release(); c->xr.release(); c->hs.release();
   c->uo.release(); c->xo.release(); c->st.release(); c->it.release();
   c->wW.release(); c->wkey.release(); c->wact.release();
+  c->lscr.release(); c->lfail.release(); c->lcnt.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -168,6 +187,35 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
   return F110QP_OK;
 }
 
+// Back end of a call and, for the lane back end, its workspace.
+static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110qp::LaneWork* lw) {
+  *lw = f110qp::LaneWork();
+  const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
+  int be = c->cfg.backend;
+  if (be == F110QP_BACKEND_AUTO) be = (!gap && batch >= F110QP_LANE_MIN_BATCH) ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
+  if (gap) be = F110QP_BACKEND_WAVE;
+  *backend = (be == F110QP_BACKEND_LANE) ? f110qp::BACKEND_LANE : f110qp::BACKEND_WAVE;
+  if (*backend != f110qp::BACKEND_LANE) return F110QP_OK;
+  const size_t waves = ((size_t)batch + 63) / 64, N = (size_t)c->cfg.horizon;
+  hipError_t e;
+  if ((e = c->lscr.ensure(waves * N * 64 * (8 * sizeof(double) + sizeof(int)))) ||
+      (e = c->lfail.ensure((size_t)batch * sizeof(int))))
+    return hip_fail(e, "hipMalloc lane workspace");
+  if (!c->lcnt.p) {
+    if ((e = c->lcnt.ensure(2 * sizeof(int))) || (e = hipMemsetAsync(c->lcnt.p, 0, 2 * sizeof(int), s)))
+      return hip_fail(e, "hipMalloc lane counters");
+  }
+  int* cnt = (int*)c->lcnt.p;
+  lw->scratch = (double*)c->lscr.p;
+  lw->fail_list = (int*)c->lfail.p;
+  lw->fail_count = cnt + c->lane_parity;
+  lw->fail_count_next = cnt + (1 - c->lane_parity);
+  lw->kmax = c->lane_kmax;
+  lw->mode = c->lane_mode;
+  c->lane_parity ^= 1;
+  return F110QP_OK;
+}
+
 int f110qp_warm_reset(f110qp_ctx* c) {
   if (!c) return fail(F110QP_ERR_INVALID, "ctx is NULL");
   c->warm_batch = 0;  // the next call re-zeroes the slot keys
@@ -183,8 +231,12 @@ int f110qp_solve_batch_dev(f110qp_ctx* c, int batch, const float* x0, const floa
   f110qp::WarmState ws;
   rc = warm_state(c, batch, (hipStream_t)stream, &ws);
   if (rc) return rc;
-  hipError_t e = f110qp::launch_solve(c->kp, batch, x0, ul, xr, h, uo, xo, st, it, ws,
-                                      (hipStream_t)stream);
+  int backend;
+  f110qp::LaneWork lw;
+  rc = lane_work(c, batch, (hipStream_t)stream, &backend, &lw);
+  if (rc) return rc;
+  hipError_t e = f110qp::launch_solve(c->kp, batch, x0, ul, xr, h, uo, xo, st, it, ws, backend,
+                                      lw, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
   return F110QP_OK;
 }
@@ -218,9 +270,14 @@ int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* u
   f110qp::WarmState ws;
   rc = warm_state(c, batch, s, &ws);
   if (rc) return rc;
+  int backend;
+  f110qp::LaneWork lw;
+  rc = lane_work(c, batch, s, &backend, &lw);
+  if (rc) return rc;
   e = f110qp::launch_solve(c->kp, batch, (const float*)c->x0.p, (const float*)c->ul.p,
                            (const float*)c->xr.p, gap ? (const float*)c->hs.p : nullptr,
-                           (float*)c->uo.p, (float*)c->xo.p, (int*)c->st.p, (int*)c->it.p, ws, s);
+                           (float*)c->uo.p, (float*)c->xo.p, (int*)c->st.p, (int*)c->it.p, ws,
+                           backend, lw, s);
   if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
   if ((e = hipMemcpyAsync(uo, c->uo.p, s_uo, hipMemcpyDeviceToHost, s)) ||
       (e = hipMemcpyAsync(xo, c->xo.p, s_xo, hipMemcpyDeviceToHost, s)) ||

@@ -35,10 +35,31 @@ struct WarmState {
   unsigned long long* act = nullptr;
 };
 
-// Solve B QPs. hs == nullptr -> box-only kernel (gap rows inactive).
+// Workspace of the lane-per-QP kernel (lane_kernel.hip): per-wave Riccati scratch
+// (ceil(B/64) x N x 8 x 64 doubles, then ceil(B/64) x N x 64 ints of PDAS state), the device-side list of QPs handed to the wave kernel and
+// two list counters used alternately by consecutive calls (each call clears the other one).
+struct LaneWork {
+  double* scratch = nullptr;
+  int* fail_list = nullptr;
+  int* fail_count = nullptr;
+  int* fail_count_next = nullptr;
+  int kmax = 16;  // PDAS passes before a QP is handed over
+  int mode = 0;   // scratch: 0 auto, 1 LDS fp64, 2 LDS fp32, 3 HBM fp64 (the workspace above)
+};
+
+enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
+
+// Solve B QPs. hs == nullptr -> box-only kernels (gap rows inactive). backend LANE (box rows
+// only): lane-per-QP Riccati/PDAS kernel, then the wave kernel on its non-converged QPs.
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u_lin,
                         const float* x_ref, const float* hs, float* u_out, float* x_out,
-                        int* status, int* iters, const WarmState& warm, hipStream_t stream);
+                        int* status, int* iters, const WarmState& warm, int backend,
+                        const LaneWork& lw, hipStream_t stream);
+
+// The lane-per-QP kernel alone (box rows).
+hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* u_lin,
+                       const float* x_ref, float* u_out, float* x_out, int* status, int* iters,
+                       const WarmState& warm, const LaneWork& lw, hipStream_t stream);
 
 // Dump the condensed H (B x 2N x 2N) and g (B x 2N) as built by the solve kernel.
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* u_lin,

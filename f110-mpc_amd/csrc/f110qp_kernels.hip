@@ -12,15 +12,19 @@ namespace f110qp {
 template <int NUM, bool GAP>
 hipError_t launch_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                     const float* hs, float* uo, float* xo, int* st, int* its, double* Hd,
-                    double* gd, const WarmState& ws, hipStream_t s);  // solve_inst.hip
+                    double* gd, const WarmState& ws, const int* list, const int* count, int grid,
+                    hipStream_t s);  // solve_inst.hip
 
 template <bool GAP>
 static hipError_t launch_g(const KParams& P, int B, const float* x0, const float* ul,
                            const float* xr, const float* hs, float* uo, float* xo, int* st,
-                           int* its, double* Hd, double* gd, const WarmState& ws, hipStream_t s) {
+                           int* its, double* Hd, double* gd, const WarmState& ws, const int* list,
+                           const int* count, int grid, hipStream_t s) {
   const int NU = 2 * P.N;
-#define F110QP_CASE(NUM) \
-  if (NU <= NUM) return launch_t<NUM, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, s);
+#define F110QP_CASE(NUM)                                                                    \
+  if (NU <= NUM)                                                                            \
+    return launch_t<NUM, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, list, count, \
+                              grid, s);
   F110QP_CASE(8) F110QP_CASE(16) F110QP_CASE(24) F110QP_CASE(32) F110QP_CASE(40)
   F110QP_CASE(48) F110QP_CASE(56) F110QP_CASE(64) F110QP_CASE(80) F110QP_CASE(96)
 #undef F110QP_CASE
@@ -29,17 +33,30 @@ static hipError_t launch_g(const KParams& P, int B, const float* x0, const float
 
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
                         const float* xr, const float* hs, float* uo, float* xo, int* st,
-                        int* its, const WarmState& ws, hipStream_t s) {
+                        int* its, const WarmState& ws, int backend, const LaneWork& lw,
+                        hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (hs) return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, s);
-  return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, s);
+  if (hs)
+    return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
+                          nullptr, B, s);
+  if (backend == BACKEND_LANE) {
+    hipError_t e = launch_lane(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+    if (e != hipSuccess) return e;
+    // the QPs whose PDAS did not settle within kmax passes: wave kernel (GI), grid-stride
+    // over the device-side list (an empty list costs one short launch)
+    const int grid = B < 256 ? B : 256;
+    return launch_g<false>(P, B, x0, ul, xr, nullptr, uo, xo, st, its, nullptr, nullptr, ws,
+                           lw.fail_list, lw.fail_count, grid, s);
+  }
+  return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
+                         nullptr, B, s);
 }
 
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* ul,
                                  const float* xr, double* Hd, double* gd, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   return launch_g<false>(P, B, x0, ul, xr, nullptr, nullptr, nullptr, nullptr, nullptr, Hd, gd,
-                         WarmState(), s);
+                         WarmState(), nullptr, nullptr, B, s);
 }
 
 }  // namespace f110qp

@@ -1,0 +1,381 @@
+// lane_kernel.hip — the throughput path: ONE LANE PER QP (64 box-constrained QPs per wave).
+//
+// The reference solves, per control tick, the sparse QP of MPC::Update (src/mpc.cpp:69-143):
+// min sum_i 1/2 |x_i - r_i|_Q^2 + 1/2 |u_i - u_des|_R^2 subject to the dynamics rows
+// x_{i+1} = A x_i + B u_i + C (mpc.cpp:244-248,299,305; A, B, C from Model::Linearize,
+// model.cpp:30-59, the same at every stage) and the input box rows (mpc.cpp:253,281,290).
+// With the gap rows inactive (the shipped bounds, mpc.cpp:296-300) that is a box-constrained
+// linear-quadratic regulator, and its exact optimum comes from a primal-dual active set on the
+// inputs where every pass is one Riccati recursion over the horizon:
+//   backward  i = N-1..0 : one Riccati step with the stage's fixed inputs masked out (branch
+//                          free): P_i = Hxx + Hux' K_i, p_i = hx + Hux' k_i
+//   forward   i = 0..N-1 : u_i = K_i x_i + k_i, x_{i+1} = A x_i + B u_i + C
+//   adjoint   i = N-1..0 : costate lambda_i = Q(x_i - r_i) + A' lambda_{i+1}; the gradient
+//                          R(u_i - u_des) + B' lambda_{i+1} gives the bound multipliers and
+//                          the PDAS re-guess of stage i (~20 flops per stage)
+// An adjoint sweep that changes nothing certifies the KKT conditions (active bounds with
+// non-negative multipliers, inactive inputs inside the box): the stored forward sweep is the
+// solution. Everything is fp64 in registers (the recursion is ~130 flops per stage), so the
+// result is the exact optimum to ~1e-12, recentred on (x0, y0) like the wave kernel.
+//
+// Layout: lane l of workgroup w solves QP b = 64 w + l. The wave's 64 reference paths are
+// contiguous in HBM; they are staged once into LDS transposed ([i][c][lane], conflict free).
+// K_i, k_i (backward -> forward) and u_i, x_i (forward -> next backward) go through a per-wave
+// HBM scratch laid out [stage][8][lane] (fully coalesced 512-B rows, L2 resident at these
+// sizes), the per-stage PDAS state through [stage][lane] ints after it. No cross-lane traffic at all except the wave-uniform "any lane still iterating" vote.
+// Lanes that have not converged after kmax passes are appended to a device-side list that the
+// wave-per-QP kernel (solve_kernel.h, GI fallback) then solves.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "f110qp_kernels.h"
+
+namespace f110qp {
+
+
+// Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
+template <typename ST, bool SLDS>
+__global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
+                                                  const float* __restrict__ x0g,
+                                                  const float* __restrict__ ulg,
+                                                  const float* __restrict__ xrg,
+                                                  float* __restrict__ uout,
+                                                  float* __restrict__ xout,
+                                                  int* __restrict__ status_out,
+                                                  int* __restrict__ iters_out,
+                                                  double* __restrict__ scr,
+                                                  int* __restrict__ fail_list,
+                                                  int* __restrict__ fail_count,
+                                                  int* __restrict__ fail_count_next,
+                                                  const WarmState ws, const int kmax) {
+  extern __shared__ __attribute__((aligned(16))) float xr_s[];  // [3N][64] x_ref, transposed
+  const int lane = threadIdx.x;
+  const int b0 = blockIdx.x * 64;
+  const int b = b0 + lane;
+  const bool live = b < B;
+  const int N = P.N;
+  const int n3 = 3 * N;
+  if (blockIdx.x == 0 && lane == 0) *fail_count_next = 0;  // the next call's list (double buffer)
+
+  // ---- stage the wave's reference paths (one contiguous block of nq * 3N floats) ----------
+  // Linear, coalesced sweep over the block (element e -> QP e / 3N, entry e % 3N), eight
+  // independent loads in flight per lane, written transposed to LDS.
+  {
+    const int nq = (B - b0) < 64 ? (B - b0) : 64;
+    const int tot = nq * n3;
+    const float* src = xrg + (size_t)b0 * n3;
+    const float rn3 = 1.0f / (float)n3;
+    for (int e0 = 0; e0 < tot; e0 += 8 * 64) {
+      float vbuf[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int e = e0 + j * 64 + lane;
+        vbuf[j] = (e < tot) ? src[e] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int e = e0 + j * 64 + lane;
+        int q = (int)((float)e * rn3);
+        q -= (q * n3 > e) ? 1 : 0;
+        q += ((q + 1) * n3 <= e) ? 1 : 0;
+        if (e < tot) xr_s[(e - q * n3) * 64 + q] = vbuf[j];
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- per-lane QP data (Model::Linearize, model.cpp:30-59; fp64 of the float inputs) ----
+  const int bb = live ? b : 0;
+  const double X0 = (double)x0g[3 * bb + 0], Y0 = (double)x0g[3 * bb + 1];
+  const float fTH0 = x0g[3 * bb + 2];
+  const double th0 = (double)fTH0;
+  const double v = (double)ulg[2 * bb + 0], d = (double)ulg[2 * bb + 1];
+  const double dt = (double)P.dt;
+  const double Lw = (double)0.3302f;
+  const double sn = sin(th0), cs = cos(th0), sd = sin(d), cd = cos(d);
+  const double sec2 = 1.0 / (cd * cd);
+  const double a02 = -1 * v * sn * dt, a12 = v * cs * dt;                  // :42-43
+  const double b00 = cs * dt, b10 = sn * dt;                               // :48-49
+  const double b20 = (sd / cd) * dt / Lw, b21 = v * sec2 * dt / Lw;        // :50-51
+  const double c0r = v * th0 * sn * dt, c1r = -1 * v * th0 * cs * dt;     // :53-54
+  const double c2 = -1 * d * v * sec2 * dt / Lw;                           // :55
+  // The state is recentred on x0 = (X0, Y0, th0): translation invariance in (x, y) and, for the
+  // heading, x_{i+1} = x_i + a02 th_i + ... + c0 = x_i + a02 (th_i - th0) + ... + (c0 + a02 th0).
+  // c0 + a02 th0 is zero up to rounding (model.cpp:42,53); keeping it as computed stays exact.
+  const double c0 = c0r + a02 * th0, c1 = c1r + a12 * th0;
+  const double q0 = P.q[0], q1 = P.q[1], q2 = P.q[2], r0 = P.r[0], r1 = P.r[1];
+  const double ud0 = P.udes[0], ud1 = P.udes[1];
+  const double lb0 = (double)P.umin[0], lb1 = (double)P.umin[1];
+  const double ub0 = (double)P.umax[0], ub1 = (double)P.umax[1];
+
+  // scratch slot (i, e) of this lane: sp[(8 i + e) * 64]; the PDAS state of stage i (2 bits
+  // per input: 0 free, 1 lower bound, 2 upper bound) at ap[i * 64]. Both live in HBM rather
+  // than registers: a per-stage state indexed by the run-time stage would spill anyway.
+  ST* sp;
+  int* ap;
+  if constexpr (SLDS) {
+    sp = reinterpret_cast<ST*>(xr_s + 3 * N * 64) + lane;
+    ap = reinterpret_cast<int*>(reinterpret_cast<ST*>(xr_s + 3 * N * 64) + (size_t)N * 8 * 64) + lane;
+  } else {
+    sp = reinterpret_cast<ST*>(scr) + (size_t)blockIdx.x * N * 8 * 64 + lane;
+    ap = reinterpret_cast<int*>(reinterpret_cast<ST*>(scr) + (size_t)gridDim.x * N * 8 * 64) +
+         (size_t)blockIdx.x * N * 64 + lane;
+  }
+  const int R = (2 * N + 63) / 64;  // register-row count of the wave kernel's act layout
+  {
+    // previous tick's active bounds seed the first pass (C5; zero masks = cold start)
+    unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
+    if (ws.act && live) {
+      lo0 = ws.act[2 * R * b];
+      hi0 = ws.act[2 * R * b + 1];
+      if (R > 1) {
+        lo1 = ws.act[2 * (R * b + 1)];
+        hi1 = ws.act[2 * (R * b + 1) + 1];
+      }
+    }
+    for (int i = 0; i < N; i++) {
+      int st = 0;
+#pragma unroll
+      for (int a = 0; a < 2; a++) {
+        const int va = 2 * i + a;
+        const unsigned long long l = va < 64 ? lo0 : lo1, h = va < 64 ? hi0 : hi1;
+        const int ca = ((l >> (va & 63)) & 1ull) ? 1 : (((h >> (va & 63)) & 1ull) ? 2 : 0);
+        st |= ca << (2 * a);
+      }
+      ap[i * 64] = st;
+    }
+  }
+  auto ref = [&](int i, double& rx, double& ry, double& rt) {
+    rx = (double)xr_s[(3 * i + 0) * 64 + lane] - X0;
+    ry = (double)xr_s[(3 * i + 1) * 64 + lane] - Y0;
+    rt = (double)xr_s[(3 * i + 2) * 64 + lane] - th0;
+  };
+
+  // Rounds: a Riccati sweep for the current active set (backward, then forward storing
+  // u_i, x_i), then a light adjoint sweep that re-guesses the set (PDAS). No change certifies
+  // the KKT conditions and the stored forward sweep is the solution.
+  bool done = !live;
+  double xN0 = 0.0, xN1 = 0.0, xN2 = 0.0;  // x_N of the last forward sweep
+  for (int pass = 0; pass < kmax; pass++) {
+    if (__ballot(!done) == 0ull) break;
+    if (!done) {
+      // ---- Riccati backward sweep ---------------------------------------------------------
+      double rx, ry, rt;
+      ref(N - 1, rx, ry, rt);  // terminal stage reuses x_ref[N-1] (mpc.cpp:228)
+      double P00 = q0, P01 = 0.0, P02 = 0.0, P11 = q1, P12 = 0.0, P22 = q2;
+      double p0 = -q0 * rx, p1 = -q1 * ry, p2 = -q2 * rt;
+      int nst = ap[(N - 1) * 64];
+      for (int i = N - 1; i >= 0; i--) {
+        ST* s = sp + (size_t)i * 8 * 64;
+        const int sti = nst;
+        if (i > 0) nst = ap[(i - 1) * 64];
+        ref(i, rx, ry, rt);
+        // Riccati step of stage i against V_{i+1}(x) = 1/2 x'Px + p'x
+        const double g0 = P00 * c0 + P01 * c1 + P02 * c2 + p0;  // P C + p
+        const double g1 = P01 * c0 + P11 * c1 + P12 * c2 + p1;
+        const double g2 = P02 * c0 + P12 * c1 + P22 * c2 + p2;
+        const double pb0 = P00 * b00 + P01 * b10 + P02 * b20;      // P B[:,0]
+        const double pb1 = P01 * b00 + P11 * b10 + P12 * b20;
+        const double pb2 = P02 * b00 + P12 * b10 + P22 * b20;
+        const double pc0 = P02 * b21, pc1 = P12 * b21, pc2 = P22 * b21;  // P B[:,1]
+        const double H00 = r0 + b00 * pb0 + b10 * pb1 + b20 * pb2;  // R + B'PB
+        const double H01 = b21 * pb2;
+        const double H11 = r1 + b21 * pc2;
+        // Hux = B'PA: row a = ((PB_a)_0, (PB_a)_1, (PB_a)_2 + a02 (PB_a)_0 + a12 (PB_a)_1)
+        const double X00 = pb0, X01 = pb1, X02 = pb2 + a02 * pb0 + a12 * pb1;
+        const double X10 = pc0, X11 = pc1, X12 = pc2 + a02 * pc0 + a12 * pc1;
+        const double h0 = -r0 * ud0 + b00 * g0 + b10 * g1 + b20 * g2;  // -R ud + B'g
+        const double h1 = -r1 * ud1 + b21 * g2;
+        // Hxx = Q + A'PA, hx = -Q r + A'g
+        const double e0 = P02 + a02 * P00 + a12 * P01, e1 = P12 + a02 * P01 + a12 * P11;
+        const double e2 = P22 + a02 * P02 + a12 * P12;
+        const double Y00 = q0 + P00, Y01 = P01, Y11 = q1 + P11, Y02 = e0, Y12 = e1;
+        const double Y22 = q2 + e2 + a02 * e0 + a12 * e1;
+        const double hx0 = -q0 * rx + g0, hx1 = -q1 * ry + g1;
+        const double hx2 = -q2 * rt + g2 + a02 * g0 + a12 * g1;
+        // masked 2x2 solve over the free inputs of the stage (fixed ones sit on their bound)
+        const int ca0 = sti & 3, ca1 = (sti >> 2) & 3;
+        const bool f0 = ca0 == 0, f1 = ca1 == 0;
+        const double bA0 = f0 ? 0.0 : (ca0 == 1 ? lb0 : ub0);
+        const double bA1 = f1 ? 0.0 : (ca1 == 1 ? lb1 : ub1);
+        const double M00 = f0 ? H00 : 1.0, M11 = f1 ? H11 : 1.0, M01 = (f0 && f1) ? H01 : 0.0;
+        const double det = M00 * M11 - M01 * M01;  // > 0: R + B'PB is positive definite
+        double idet = __builtin_amdgcn_rcp(det);   // + two Newton steps: full fp64
+        idet = fma(idet, fma(-det, idet, 1.0), idet);
+        idet = fma(idet, fma(-det, idet, 1.0), idet);
+        const double I00 = f0 ? M11 * idet : 0.0, I11 = f1 ? M00 * idet : 0.0;
+        const double I01 = (f0 && f1) ? -M01 * idet : 0.0;
+        const double K00 = -(I00 * X00 + I01 * X10), K01 = -(I00 * X01 + I01 * X11);
+        const double K02 = -(I00 * X02 + I01 * X12);
+        const double K10 = -(I01 * X00 + I11 * X10), K11 = -(I01 * X01 + I11 * X11);
+        const double K12 = -(I01 * X02 + I11 * X12);
+        const double w0 = h0 + H00 * bA0 + H01 * bA1, w1 = h1 + H01 * bA0 + H11 * bA1;
+        const double k0 = bA0 - (I00 * w0 + I01 * w1), k1 = bA1 - (I01 * w0 + I11 * w1);
+        s[0] = (ST)K00; s[64] = (ST)K01; s[128] = (ST)K02; s[192] = (ST)K10; s[256] = (ST)K11;
+        s[320] = (ST)K12; s[384] = (ST)k0; s[448] = (ST)k1;
+        // V_i: P = Hxx + Hux' K, p = hx + Hux' k
+        P00 = Y00 + X00 * K00 + X10 * K10;
+        P01 = Y01 + X00 * K01 + X10 * K11;
+        P02 = Y02 + X00 * K02 + X10 * K12;
+        P11 = Y11 + X01 * K01 + X11 * K11;
+        P12 = Y12 + X01 * K02 + X11 * K12;
+        P22 = Y22 + X02 * K02 + X12 * K12;
+        p0 = hx0 + X00 * k0 + X10 * k1;
+        p1 = hx1 + X01 * k0 + X11 * k1;
+        p2 = hx2 + X02 * k0 + X12 * k1;
+      }
+      // ---- forward sweep: u_i = K_i x_i + k_i, x_{i+1} = A x_i + B u_i + C --------------
+      {
+        double x0 = 0.0, x1 = 0.0, x2 = 0.0;  // recentred x_0
+        double K00 = sp[0], K01 = sp[64], K02 = sp[128], K10 = sp[192], K11 = sp[256];
+        double K12 = sp[320], k0 = sp[384], k1 = sp[448];  // stage 0; later stages prefetched
+        for (int i = 0; i < N; i++) {
+          ST* s = sp + (size_t)i * 8 * 64;
+          const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
+          const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
+          if (i + 1 < N) {
+            const ST* sn = s + 8 * 64;
+            K00 = sn[0]; K01 = sn[64]; K02 = sn[128]; K10 = sn[192]; K11 = sn[256];
+            K12 = sn[320]; k0 = sn[384]; k1 = sn[448];
+          }
+          s[0] = (ST)u0; s[64] = (ST)u1; s[128] = (ST)x0; s[192] = (ST)x1; s[256] = (ST)x2;
+          const double nx0 = x0 + a02 * x2 + b00 * u0 + c0;
+          const double nx1 = x1 + a12 * x2 + b10 * u0 + c1;
+          const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
+          x0 = nx0; x1 = nx1; x2 = nx2;
+        }
+        xN0 = x0; xN1 = x1; xN2 = x2;
+      }
+      // ---- adjoint sweep: bound multipliers and the PDAS re-guess -------------------------
+      bool changed = false;
+      {
+        ref(N - 1, rx, ry, rt);
+        double l0 = q0 * (xN0 - rx), l1 = q1 * (xN1 - ry), l2 = q2 * (xN2 - rt);  // costate
+        const ST* s = sp + (size_t)(N - 1) * 8 * 64;
+        double nu0 = s[0], nu1 = s[64], nx0 = s[128], nx1 = s[192], nx2 = s[256];
+        int nst = ap[(N - 1) * 64];
+        for (int i = N - 1; i >= 0; i--) {
+          const double u0 = nu0, u1 = nu1, x0 = nx0, x1 = nx1, x2 = nx2;
+          const int old = nst;
+          if (i > 0) {
+            const ST* sn = sp + (size_t)(i - 1) * 8 * 64;
+            nu0 = sn[0]; nu1 = sn[64]; nx0 = sn[128]; nx1 = sn[192]; nx2 = sn[256];
+            nst = ap[(i - 1) * 64];
+          }
+          ref(i, rx, ry, rt);
+          // gradient of the objective in u_i: g = R(u - ud) + B' lambda_{i+1}
+          const double g0 = r0 * (u0 - ud0) + b00 * l0 + b10 * l1 + b20 * l2;
+          const double g1 = r1 * (u1 - ud1) + b21 * l2;
+          // PDAS re-guess (Hintermueller-Ito-Kunisch, c = 1), both inputs of the stage: the
+          // multiplier of an active lower bound is g, of an active upper bound -g
+          int st = 0;
+#pragma unroll
+          for (int a = 0; a < 2; a++) {
+            const int ca = (old >> (2 * a)) & 3;
+            const double u = a ? u1 : u0, g = a ? g1 : g0;
+            const double lb = a ? lb1 : lb0, ub = a ? ub1 : ub0;
+            const bool nlo = ((ca == 1) ? g : 0.0) + (lb - u) > 0.0;
+            const bool nhi = !nlo && (((ca == 2) ? -g : 0.0) + (u - ub) > 0.0);
+            st |= (nlo ? 1 : (nhi ? 2 : 0)) << (2 * a);
+          }
+          if (st != old) {
+            changed = true;
+            ap[i * 64] = st;
+          }
+          // lambda_i = Q(x_i - r_i) + A' lambda_{i+1}  (A = I + E, E only in column 2)
+          const double nl2 = l2 + a02 * l0 + a12 * l1;
+          l0 = q0 * (x0 - rx) + l0;
+          l1 = q1 * (x1 - ry) + l1;
+          l2 = q2 * (x2 - rt) + nl2;
+        }
+      }
+      if (!changed) {
+        // KKT point: write (u*, x*) from the stored forward sweep
+        float* uo = uout + (size_t)b * 2 * N;
+        float* xo = xout + (size_t)b * 3 * (N + 1);
+        xo[0] = x0g[3 * b + 0];  // x*_0 = x0 exactly, as the dynamics rows fix it
+        xo[1] = x0g[3 * b + 1];
+        xo[2] = fTH0;
+        for (int i = 0; i < N; i++) {
+          const ST* s = sp + (size_t)i * 8 * 64;
+          uo[2 * i] = (float)(double)s[0];
+          uo[2 * i + 1] = (float)(double)s[64];
+          if (i > 0) {
+            xo[3 * i] = (float)((double)s[128] + X0);
+            xo[3 * i + 1] = (float)((double)s[192] + Y0);
+            xo[3 * i + 2] = (float)((double)s[256] + th0);
+          }
+        }
+        xo[3 * N] = (float)(xN0 + X0);
+        xo[3 * N + 1] = (float)(xN1 + Y0);
+        xo[3 * N + 2] = (float)(xN2 + th0);
+        status_out[b] = F110QP_SOLVED_ID;
+        if (iters_out) iters_out[b] = pass;  // active-set changes before the KKT point
+        done = true;
+      }
+    }
+  }
+  if (live && ws.act && done) {  // active set of this solution for the next tick
+    unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
+    for (int i = 0; i < N; i++) {
+      const int st = ap[i * 64];
+#pragma unroll
+      for (int a = 0; a < 2; a++) {
+        const int va = 2 * i + a, ca = (st >> (2 * a)) & 3;
+        const unsigned long long bit = 1ull << (va & 63);
+        const unsigned long long in0 = va < 64 ? bit : 0ull, in1 = va < 64 ? 0ull : bit;
+        lo0 |= (ca == 1) ? in0 : 0ull;
+        lo1 |= (ca == 1) ? in1 : 0ull;
+        hi0 |= (ca == 2) ? in0 : 0ull;
+        hi1 |= (ca == 2) ? in1 : 0ull;
+      }
+    }
+    ws.act[2 * R * b] = lo0;
+    ws.act[2 * R * b + 1] = hi0;
+    if (R > 1) {
+      ws.act[2 * (R * b + 1)] = lo1;
+      ws.act[2 * (R * b + 1) + 1] = hi1;
+    }
+  }
+  if (live && !done) fail_list[atomicAdd(fail_count, 1)] = b;  // -> wave kernel (GI)
+}
+
+template <typename ST, bool SLDS>
+static hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul,
+                                const float* xr, float* uo, float* xo, int* st, int* its,
+                                const WarmState& ws, const LaneWork& lw, size_t lds,
+                                hipStream_t s) {
+  const int waves = (B + 63) / 64;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_kernel<ST, SLDS>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((lane_kernel<ST, SLDS>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr,
+                     uo, xo, st, its, lw.scratch, lw.fail_list, lw.fail_count,
+                     lw.fail_count_next, ws, lw.kmax);
+  return hipGetLastError();
+}
+
+// LDS per wave: the staged references (12 N * 64 B) + Riccati scratch (8 N * 64 * sizeof(ST))
+// + PDAS state (4 N * 64 B) (lane_mode 0 = auto; 1/2/3 force LDS fp64 / LDS fp32 / HBM fp64).
+hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* ul,
+                       const float* xr, float* uo, float* xo, int* st, int* its,
+                       const WarmState& ws, const LaneWork& lw, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  const size_t N = (size_t)P.N;
+  const size_t base = N * 64 * (12 + 4);
+  const size_t lds64 = base + N * 8 * 64 * sizeof(double), lds32 = base + N * 8 * 64 * sizeof(float);
+  const size_t cap = 160 * 1024;
+  int mode = lw.mode;
+  // auto: fp64 scratch in LDS while one wave per CU covers the batch (latency), else the HBM
+  // workspace (occupancy; the recursion is VALU-issue bound, not memory bound)
+  if (mode == 0) mode = (lds64 <= cap && (B + 63) / 64 <= 256) ? 1 : 3;
+  if (mode == 1 && lds64 <= cap)
+    return launch_lane_t<double, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds64, s);
+  if (mode == 2 && lds32 <= cap)
+    return launch_lane_t<float, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds32, s);
+  return launch_lane_t<double, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, N * 12 * 64, s);
+}
+
+}  // namespace f110qp

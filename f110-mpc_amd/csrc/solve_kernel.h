@@ -582,22 +582,19 @@ __device__ __forceinline__ int build_box_slots(Smem<NUM, GAP>& sm, int lane, con
 }
 
 template <int NUM, bool GAP>
-__global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
-                                                   const float* __restrict__ x0g,
-                                                   const float* __restrict__ ulg,
-                                                   const float* __restrict__ xrg,
-                                                   const float* __restrict__ hsg,
-                                                   float* __restrict__ uout,
-                                                   float* __restrict__ xout,
-                                                   int* __restrict__ status_out,
-                                                   int* __restrict__ iters_out,
-                                                   double* __restrict__ Hdbg,
-                                                   double* __restrict__ gdbg,
-                                                   const WarmState ws) {
+__device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const KParams& P,
+                                         const float* __restrict__ x0g,
+                                         const float* __restrict__ ulg,
+                                         const float* __restrict__ xrg,
+                                         const float* __restrict__ hsg,
+                                         float* __restrict__ uout,
+                                         float* __restrict__ xout,
+                                         int* __restrict__ status_out,
+                                         int* __restrict__ iters_out,
+                                         double* __restrict__ Hdbg,
+                                         double* __restrict__ gdbg,
+                                         const WarmState& ws) {
   constexpr int R = (NUM + 63) / 64;
-  __shared__ Smem<NUM, GAP> sm;
-  const int b = blockIdx.x;
-  if (b >= B) return;
   const int lane = threadIdx.x;
   const int N = P.N;
   const int NU = 2 * N;
@@ -1412,15 +1409,43 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
 #endif
 }
 
+// One QP per workgroup (= one wave). With `list` the grid walks the index list instead
+// (count read on the device): the lane-per-QP kernel hands its non-converged QPs over this way.
+template <int NUM, bool GAP>
+__global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
+                                                   const float* __restrict__ x0g,
+                                                   const float* __restrict__ ulg,
+                                                   const float* __restrict__ xrg,
+                                                   const float* __restrict__ hsg,
+                                                   float* __restrict__ uout,
+                                                   float* __restrict__ xout,
+                                                   int* __restrict__ status_out,
+                                                   int* __restrict__ iters_out,
+                                                   double* __restrict__ Hdbg,
+                                                   double* __restrict__ gdbg,
+                                                   const WarmState ws,
+                                                   const int* __restrict__ list,
+                                                   const int* __restrict__ count) {
+  __shared__ Smem<NUM, GAP> sm;
+  const int n = list ? __builtin_amdgcn_readfirstlane(*count) : B;
+  for (int item = blockIdx.x; item < n; item += gridDim.x) {
+    const int b = list ? __builtin_amdgcn_readfirstlane(list[item]) : item;
+    solve_qp<NUM, GAP>(sm, b, P, x0g, ulg, xrg, hsg, uout, xout, status_out, iters_out, Hdbg,
+                       gdbg, ws);
+    wsync();
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // launch of one instantiation
 // ------------------------------------------------------------------------------------------
 template <int NUM, bool GAP>
 hipError_t launch_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                     const float* hs, float* uo, float* xo, int* st, int* its, double* Hd,
-                    double* gd, const WarmState& ws, hipStream_t s) {
-  hipLaunchKernelGGL((solve_kernel<NUM, GAP>), dim3(B), dim3(64), 0, s, P, B, x0, ul, xr, hs, uo,
-                     xo, st, its, Hd, gd, ws);
+                    double* gd, const WarmState& ws, const int* list, const int* count, int grid,
+                    hipStream_t s) {
+  hipLaunchKernelGGL((solve_kernel<NUM, GAP>), dim3(grid), dim3(64), 0, s, P, B, x0, ul, xr, hs,
+                     uo, xo, st, its, Hd, gd, ws, list, count);
   return hipGetLastError();
 }
 

@@ -25,6 +25,10 @@ PRIMAL_INFEASIBLE = -3
 NUMERICAL = -10
 GAP_INACTIVE = 0
 GAP_ACTIVE = 1
+BACKEND_AUTO = 0
+BACKEND_WAVE = 1
+BACKEND_LANE = 2
+LANE_MIN_BATCH = 2048
 MAX_HORIZON = 48
 
 # every symbol include/f110qp.h declares
@@ -56,6 +60,7 @@ class Config(C.Structure):
         ("max_iter", C.c_int),
         ("device", C.c_int),
         ("warm_start", C.c_int),
+        ("backend", C.c_int),
     ]
 
 

@@ -20,7 +20,8 @@
  *  - The caller owns every buffer. *_dev entry points take device pointers and a
  *    hipStream_t (passed as void*) and are asynchronous on that stream; the host-pointer
  *    entry points are synchronous.
- *  - One f110qp_ctx per host thread. A ctx owns its device workspace.
+ *  - One f110qp_ctx per host thread. A ctx owns its device workspace, so the calls made on
+ *    one ctx must be ordered (one stream, or synchronised between streams).
  *  - Layouts (row-major, float32):
  *      x0        [B][3]      (x, y, ori)           State  (include/f110-mpc/state.h:10-45)
  *      u_lin     [B][2]      (v, steer_ang)        Input  (include/f110-mpc/input.h:11-34)
@@ -40,7 +41,7 @@
 extern "C" {
 #endif
 
-#define F110QP_API_VERSION 1
+#define F110QP_API_VERSION 2
 
 /* return codes */
 #define F110QP_OK 0
@@ -57,6 +58,13 @@ extern "C" {
 /* gap (follow-the-gap half-space) row semantics, src/mpc.cpp:279-300 */
 #define F110QP_GAP_INACTIVE 0     /* as shipped: gap rows bounded by +-OsqpEigen::INFTY */
 #define F110QP_GAP_ACTIVE 1       /* a*x+b*y >= -(c+0.5) on stages 1..N (mpc.cpp:297-298) */
+
+/* solver back ends (f110qp_config.backend) */
+#define F110QP_BACKEND_AUTO 0     /* lane-per-QP for box-only batches >= F110QP_LANE_MIN_BATCH */
+#define F110QP_BACKEND_WAVE 1     /* one wavefront per QP: condensed W = H^-1 + PDAS/GI        */
+#define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64 (box rows only;     */
+                                  /* gap rows always use the wave back end)                   */
+#define F110QP_LANE_MIN_BATCH 2048
 
 #define F110QP_MAX_HORIZON 48  /* 2N <= 96 decision variables: two register rows per lane */
 
@@ -78,6 +86,7 @@ typedef struct {
                     /*    linearisation point (theta0, v, steer) is bit-identical to its    */
                     /*    previous call's, and the previous active set seeds the solve.    */
                     /*    Slot b of call t+1 continues slot b of call t (same batch size). */
+  int backend;      /* F110QP_BACKEND_AUTO | _WAVE | _LANE (both give the exact optimum)    */
 } f110qp_config;
 
 /* Library / ABI version (F110QP_API_VERSION). */

@@ -30,7 +30,7 @@ def test_library_is_gfx950_code_object(capi):
 
 def test_version_and_defaults(capi):
     L = capi.load()
-    assert L.f110qp_version() == 1
+    assert L.f110qp_version() == 2
     c = capi.default_config(20)
     # params.yaml:1-13,42-47 and constraints.cpp:19,21
     assert c.horizon == 20 and c.dt == np.float32(0.01)
@@ -38,12 +38,13 @@ def test_version_and_defaults(capi):
     assert list(c.u_des) == [4.5, 0.0]
     assert list(c.u_min) == [3.0, float(np.float32(-0.43))]
     assert list(c.u_max) == [4.5, float(np.float32(0.43))]
-    assert c.gap_mode == capi.GAP_INACTIVE
+    assert c.gap_mode == capi.GAP_INACTIVE and c.backend == capi.BACKEND_AUTO
 
 
 @pytest.mark.parametrize("over,msg", [
     (dict(horizon=0), "horizon"),
     (dict(horizon=49), "horizon"),
+    (dict(backend=3), "backend"),
     (dict(r=[0.0, 5.0]), "R must be > 0"),
     (dict(q=[-1.0, 10.0, 0.0]), "Q must be"),
     (dict(u_min=[5.0, -0.43]), "u_min > u_max"),

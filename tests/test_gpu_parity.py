@@ -33,8 +33,8 @@ def halfspaces_oracle(oracle, x0, ranges, geom):
     return hs
 
 
-def check(oracle, capi, N, w, hs=None, gap=False, tol=TOL):
-    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE))
+def check(oracle, capi, N, w, hs=None, gap=False, tol=TOL, **cfg):
+    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, **cfg))
     u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
     s.close()
     ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=gap)
@@ -348,3 +348,97 @@ def test_warm_started_stream_horizon40(oracle, capi):
         np.testing.assert_array_equal(sw, sr)
         assert rel_err(uw, ur).max() <= TOL and rel_err(xw, xr).max() <= TOL
     warm.close()
+
+
+# ---- lane-per-QP back end (Riccati/PDAS, fp64) ------------------------------------------------
+
+@pytest.mark.parametrize("N", [1, 2, 5, 17, 20, 30, 32, 33, 40, 48])
+def test_lane_backend_horizons(oracle, capi, N):
+    """The lane back end (one QP per lane) against the exact optimum; batch not a multiple of
+    64 so the last wave is partial."""
+    w = workload.make_batch(1000, N, seed=700 + N, lateral=0.6)
+    u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
+    assert (st == capi.SOLVED).all()
+
+
+@pytest.mark.parametrize("N", [20, 40])
+def test_lane_backend_hard_references(oracle, capi, N):
+    """True-heading references with big offsets and steer beyond the box: many active bounds
+    on both faces, several PDAS passes."""
+    w = workload.make_batch(2048, N, seed=770 + N, heading="true", lateral=2.0, steer_range=1.2)
+    u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
+    assert it.max() >= 2
+
+
+def test_lane_backend_custom_weights_and_far_origin(oracle, capi):
+    N = 20
+    over = dict(q=[3.0, 7.0, 2.0], r=[0.5, 1.5], u_des=[3.7, 0.05], u_min=[3.5, -0.2], u_max=[4.0, 0.2])
+    w = workload.make_batch(640, N, seed=881, lateral=0.7)
+    w["x0"][:, :2] += np.float32(1000.0)
+    w["x_ref"][:, :, :2] += np.float32(1000.0)
+    s = capi.Solver(capi.default_config(N, backend=capi.BACKEND_LANE, **over))
+    u, x, st, _ = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    ur, xr, sr = oracle.solve_batch(oracle.params(N, **over), w["x0"], w["u_lin"], w["x_ref"])
+    np.testing.assert_array_equal(st, sr)
+    assert rel_err(u, ur).max() <= TOL and rel_err(x, xr).max() <= TOL
+
+
+def test_lane_backend_hands_over_to_wave_kernel(oracle, capi, monkeypatch):
+    """F110QP_LANE_KMAX=1 lets no QP with an active bound settle in the lane kernel: those go
+    through the device-side list to the wave kernel (GI). Results stay exact, and a second call
+    on the same context reuses the other list counter."""
+    monkeypatch.setenv("F110QP_LANE_KMAX", "1")
+    N = 20
+    w = workload.make_batch(3000, N, seed=991, heading="true", lateral=1.5, steer_range=1.0)
+    s = capi.Solver(capi.default_config(N, backend=capi.BACKEND_LANE))
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"])
+    for _ in range(3):
+        u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+        np.testing.assert_array_equal(st, sr)
+        assert rel_err(u, ur).max() <= TOL and rel_err(x, xr).max() <= TOL
+    s.close()
+
+
+def test_lane_and_wave_backends_agree(capi):
+    N, B = 20, 4096
+    w = workload.make_batch(B, N, seed=1234, heading="true", lateral=1.0)
+    res = []
+    for be in (capi.BACKEND_WAVE, capi.BACKEND_LANE, capi.BACKEND_AUTO):
+        s = capi.Solver(capi.default_config(N, backend=be))
+        res.append(s.solve(w["x0"], w["u_lin"], w["x_ref"]))
+        s.close()
+    for r in res[1:]:
+        np.testing.assert_array_equal(r[2], res[0][2])
+        assert rel_err(r[0], res[0][0].astype(np.float64)).max() <= 1e-5
+        assert rel_err(r[1], res[0][1].astype(np.float64)).max() <= 1e-5
+
+
+def test_lane_backend_warm_stream(oracle, capi):
+    """Config C5 on the lane back end: the previous tick's active set seeds PDAS."""
+    N, B, T = 20, 4096, 5
+    stream = workload.make_stream(B, N, T, seed=31, heading_change_every=2)
+    warm = capi.Solver(capi.default_config(N, warm_start=1, backend=capi.BACKEND_LANE))
+    its = []
+    for t, w in enumerate(stream):
+        u, x, st, it = warm.solve(w["x0"], w["u_lin"], w["x_ref"])
+        ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"])
+        np.testing.assert_array_equal(st, sr)
+        assert rel_err(u, ur).max() <= TOL and rel_err(x, xr).max() <= TOL, t
+        its.append(it.mean())
+    assert np.mean(its[1:]) <= its[0]
+    warm.close()
+
+
+def test_lane_backend_c4_shard(oracle, capi):
+    """BASELINE configs[3] at N = 40 through the lane back end (auto-selected at this size)."""
+    N, B = 40, 8192
+    g = workload.make_grouped_batch(69, N, seed=4041)
+    w = {k: np.ascontiguousarray(g[k][:B]) for k in ("x0", "u_lin", "x_ref")}
+    s = capi.Solver(capi.default_config(N))
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    assert (st == capi.SOLVED).all()
+    idx = np.concatenate([np.arange(0, B, 29), np.arange(480, 720)])
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
+    assert rel_err(u[idx], ur).max() <= TOL and rel_err(x[idx], xr).max() <= TOL
