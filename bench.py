@@ -242,7 +242,8 @@ def main():
     backend = {"auto": capi.BACKEND_AUTO, "wave": capi.BACKEND_WAVE, "lane": capi.BACKEND_LANE}[args.backend]
     cfg = capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, device=dev.index,
                               warm_start=int(warm), backend=backend)
-    lane = (not gap) and (backend == capi.BACKEND_LANE or (backend == capi.BACKEND_AUTO and Bper >= capi.LANE_MIN_BATCH))
+    eff = capi.auto_backend(N, Bper, gap) if backend == capi.BACKEND_AUTO else backend
+    be_name = "lane" if (eff == capi.BACKEND_LANE and not gap) else "wave"
     solver = capi.Solver(cfg)
     stream = torch.cuda.current_stream(dev)
     tick = [0]
@@ -333,7 +334,7 @@ def main():
             "horizon": N,
             "gap_rows": bool(gap),
             "warm_start": bool(warm),
-            "backend": "lane-per-QP (Riccati/PDAS fp64)" if lane else "wave-per-QP (condensed, PDAS/GI)",
+            "backend": {"wave": "wave-per-QP (condensed, PDAS/GI)", "lane": "lane-per-QP (Riccati/PDAS fp64)"}[be_name],
             "parallelism": f"independent QP shards x{world} (no collective)"
                            + (f", scenario-aligned ({GROUP}) split of one global batch" if strong else ""),
             "solved_fraction": solved,
@@ -347,7 +348,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "f110qp::lane_kernel (+ solve_kernel hand-over launch)" if lane else "f110qp::solve_kernel",
+            "kernel": {"wave": "f110qp::solve_kernel",
+                       "lane": "f110qp::lane_kernel (+ solve_kernel hand-over launch)"}[be_name],
             "kernel_ms_per_launch": kms,
             "algorithmic_bytes_per_qp": bpq,
             "fp32_compute": {"achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -192,10 +192,13 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   *lw = f110qp::LaneWork();
   const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
   int be = c->cfg.backend;
-  if (be == F110QP_BACKEND_AUTO) be = (!gap && batch >= F110QP_LANE_MIN_BATCH) ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
+  if (be == F110QP_BACKEND_AUTO) {
+    const int min_b = c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH : F110QP_LANE_MIN_BATCH_WIDE;
+    be = (!gap && batch >= min_b) ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
+  }
   if (gap) be = F110QP_BACKEND_WAVE;
   *backend = (be == F110QP_BACKEND_LANE) ? f110qp::BACKEND_LANE : f110qp::BACKEND_WAVE;
-  if (*backend != f110qp::BACKEND_LANE) return F110QP_OK;
+  if (*backend == f110qp::BACKEND_WAVE) return F110QP_OK;
   const size_t waves = ((size_t)batch + 63) / 64, N = (size_t)c->cfg.horizon;
   hipError_t e;
   if ((e = c->lscr.ensure(waves * N * 64 * (8 * sizeof(double) + sizeof(int)))) ||

@@ -32,6 +32,18 @@
 
 namespace f110qp {
 
+// Diagnostic build only (-DF110QP_STAMPS): per-wave cycles of each sweep type, read back with
+// f110qp_read_lane_stamps(). The shipped library never executes a stamp.
+#ifdef F110QP_STAMPS
+constexpr int kLaneStampSlots = 8;
+__device__ unsigned long long g_lstamps[4096 * kLaneStampSlots];
+#define LSTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define LACC(acc, since) acc += __builtin_amdgcn_s_memtime() - (since)
+#else
+#define LSTAMP(var)
+#define LACC(acc, since)
+#endif
+
 
 // Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
 template <typename ST, bool SLDS>
@@ -49,6 +61,10 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                                                   int* __restrict__ fail_count_next,
                                                   const WarmState ws, const int kmax) {
   extern __shared__ __attribute__((aligned(16))) float xr_s[];  // [3N][64] x_ref, transposed
+  LSTAMP(t_start);
+#ifdef F110QP_STAMPS
+  unsigned long long acc_bw = 0, acc_fw = 0, acc_adj = 0, acc_out = 0, t_setup = 0, npass = 0;
+#endif
   const int lane = threadIdx.x;
   const int b0 = blockIdx.x * 64;
   const int b = b0 + lane;
@@ -156,8 +172,15 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
   // the KKT conditions and the stored forward sweep is the solution.
   bool done = !live;
   double xN0 = 0.0, xN1 = 0.0, xN2 = 0.0;  // x_N of the last forward sweep
+#ifdef F110QP_STAMPS
+  t_setup = __builtin_amdgcn_s_memtime() - t_start;
+#endif
   for (int pass = 0; pass < kmax; pass++) {
     if (__ballot(!done) == 0ull) break;
+#ifdef F110QP_STAMPS
+    npass++;
+#endif
+    LSTAMP(t_bw);
     if (!done) {
       // ---- Riccati backward sweep ---------------------------------------------------------
       double rx, ry, rt;
@@ -224,6 +247,8 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         p1 = hx1 + X01 * k0 + X11 * k1;
         p2 = hx2 + X02 * k0 + X12 * k1;
       }
+      LACC(acc_bw, t_bw);
+      LSTAMP(t_fw);
       // ---- forward sweep: u_i = K_i x_i + k_i, x_{i+1} = A x_i + B u_i + C --------------
       {
         double x0 = 0.0, x1 = 0.0, x2 = 0.0;  // recentred x_0
@@ -246,6 +271,8 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         }
         xN0 = x0; xN1 = x1; xN2 = x2;
       }
+      LACC(acc_fw, t_fw);
+      LSTAMP(t_adj);
       // ---- adjoint sweep: bound multipliers and the PDAS re-guess -------------------------
       bool changed = false;
       {
@@ -289,6 +316,8 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
           l2 = q2 * (x2 - rt) + nl2;
         }
       }
+      LACC(acc_adj, t_adj);
+      LSTAMP(t_out);
       if (!changed) {
         // KKT point: write (u*, x*) from the stored forward sweep
         float* uo = uout + (size_t)b * 2 * N;
@@ -313,6 +342,7 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         if (iters_out) iters_out[b] = pass;  // active-set changes before the KKT point
         done = true;
       }
+      LACC(acc_out, t_out);
     }
   }
   if (live && ws.act && done) {  // active set of this solution for the next tick
@@ -338,6 +368,13 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
     }
   }
   if (live && !done) fail_list[atomicAdd(fail_count, 1)] = b;  // -> wave kernel (GI)
+#ifdef F110QP_STAMPS
+  if (lane == 0 && blockIdx.x < 4096) {
+    unsigned long long* o = g_lstamps + (size_t)blockIdx.x * kLaneStampSlots;
+    o[0] = t_setup; o[1] = acc_bw; o[2] = acc_fw; o[3] = acc_adj; o[4] = acc_out;
+    o[5] = npass; o[6] = __builtin_amdgcn_s_memtime() - t_start; o[7] = 0;
+  }
+#endif
 }
 
 template <typename ST, bool SLDS>
@@ -379,3 +416,10 @@ hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* ul
 }
 
 }  // namespace f110qp
+
+#ifdef F110QP_STAMPS
+extern "C" int f110qp_read_lane_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(f110qp::g_lstamps),
+                                  (size_t)n * f110qp::kLaneStampSlots * sizeof(unsigned long long));
+}
+#endif

@@ -28,7 +28,14 @@ GAP_ACTIVE = 1
 BACKEND_AUTO = 0
 BACKEND_WAVE = 1
 BACKEND_LANE = 2
-LANE_MIN_BATCH = 2048
+LANE_MIN_BATCH = 4096
+LANE_MIN_BATCH_WIDE = 512
+
+
+def auto_backend(horizon: int, batch: int, gap: bool) -> int:
+    """The back end BACKEND_AUTO resolves to (mirrors lane_work() in f110qp_api.cpp)."""
+    min_b = LANE_MIN_BATCH if horizon <= 32 else LANE_MIN_BATCH_WIDE
+    return BACKEND_LANE if (not gap and batch >= min_b) else BACKEND_WAVE
 MAX_HORIZON = 48
 
 # every symbol include/f110qp.h declares

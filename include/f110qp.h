@@ -61,10 +61,12 @@ extern "C" {
 
 /* solver back ends (f110qp_config.backend) */
 #define F110QP_BACKEND_AUTO 0     /* lane-per-QP for box-only batches >= F110QP_LANE_MIN_BATCH */
+                                  /* (N <= 32) or >= F110QP_LANE_MIN_BATCH_WIDE (N > 32)      */
 #define F110QP_BACKEND_WAVE 1     /* one wavefront per QP: condensed W = H^-1 + PDAS/GI        */
 #define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64 (box rows only;     */
                                   /* gap rows always use the wave back end)                   */
-#define F110QP_LANE_MIN_BATCH 2048
+#define F110QP_LANE_MIN_BATCH 4096       /* measured wave/lane crossover on MI355X, N = 20 */
+#define F110QP_LANE_MIN_BATCH_WIDE 512   /* N > 32 (two register rows in the wave kernel)  */
 
 #define F110QP_MAX_HORIZON 48  /* 2N <= 96 decision variables: two register rows per lane */
 

@@ -106,3 +106,13 @@ def test_capi_raises_when_library_missing(monkeypatch):
     monkeypatch.setattr(capi, "LIB_PATH", "/nonexistent/libf110qp.so")
     with pytest.raises(capi.F110QPError, match="not built"):
         capi.load()
+
+
+def test_auto_backend_policy(capi):
+    """BACKEND_AUTO: the wave kernel for small box batches and for gap rows, the lane kernel
+    from the measured crossover (4,096 QPs at N <= 32, 512 at N > 32)."""
+    assert capi.auto_backend(20, 1024, False) == capi.BACKEND_WAVE
+    assert capi.auto_backend(20, 4096, False) == capi.BACKEND_LANE
+    assert capi.auto_backend(20, 65536, True) == capi.BACKEND_WAVE
+    assert capi.auto_backend(40, 512, False) == capi.BACKEND_LANE
+    assert capi.auto_backend(40, 256, False) == capi.BACKEND_WAVE

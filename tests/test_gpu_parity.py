@@ -352,31 +352,41 @@ def test_warm_started_stream_horizon40(oracle, capi):
 
 # ---- lane-per-QP back end (Riccati/PDAS, fp64) ------------------------------------------------
 
+RICCATI = ["lane"]
+
+
+def _be(capi, name):
+    return {"lane": capi.BACKEND_LANE, "wave": capi.BACKEND_WAVE}[name]
+
+
+@pytest.mark.parametrize("be", RICCATI)
 @pytest.mark.parametrize("N", [1, 2, 5, 17, 20, 30, 32, 33, 40, 48])
-def test_lane_backend_horizons(oracle, capi, N):
-    """The lane back end (one QP per lane) against the exact optimum; batch not a multiple of
-    64 so the last wave is partial."""
+def test_lane_backend_horizons(oracle, capi, N, be):
+    """The Riccati back end (one QP per lane) against the exact optimum; batch not
+    a multiple of 64 so the last wave is partial."""
     w = workload.make_batch(1000, N, seed=700 + N, lateral=0.6)
-    u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
+    u, x, st, it = check(oracle, capi, N, w, backend=_be(capi, be))
     assert (st == capi.SOLVED).all()
 
 
+@pytest.mark.parametrize("be", RICCATI)
 @pytest.mark.parametrize("N", [20, 40])
-def test_lane_backend_hard_references(oracle, capi, N):
+def test_lane_backend_hard_references(oracle, capi, N, be):
     """True-heading references with big offsets and steer beyond the box: many active bounds
     on both faces, several PDAS passes."""
     w = workload.make_batch(2048, N, seed=770 + N, heading="true", lateral=2.0, steer_range=1.2)
-    u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
+    u, x, st, it = check(oracle, capi, N, w, backend=_be(capi, be))
     assert it.max() >= 2
 
 
-def test_lane_backend_custom_weights_and_far_origin(oracle, capi):
+@pytest.mark.parametrize("be", RICCATI)
+def test_lane_backend_custom_weights_and_far_origin(oracle, capi, be):
     N = 20
     over = dict(q=[3.0, 7.0, 2.0], r=[0.5, 1.5], u_des=[3.7, 0.05], u_min=[3.5, -0.2], u_max=[4.0, 0.2])
     w = workload.make_batch(640, N, seed=881, lateral=0.7)
     w["x0"][:, :2] += np.float32(1000.0)
     w["x_ref"][:, :, :2] += np.float32(1000.0)
-    s = capi.Solver(capi.default_config(N, backend=capi.BACKEND_LANE, **over))
+    s = capi.Solver(capi.default_config(N, backend=_be(capi, be), **over))
     u, x, st, _ = s.solve(w["x0"], w["u_lin"], w["x_ref"])
     s.close()
     ur, xr, sr = oracle.solve_batch(oracle.params(N, **over), w["x0"], w["u_lin"], w["x_ref"])
@@ -384,14 +394,15 @@ def test_lane_backend_custom_weights_and_far_origin(oracle, capi):
     assert rel_err(u, ur).max() <= TOL and rel_err(x, xr).max() <= TOL
 
 
-def test_lane_backend_hands_over_to_wave_kernel(oracle, capi, monkeypatch):
+@pytest.mark.parametrize("be", RICCATI)
+def test_lane_backend_hands_over_to_wave_kernel(oracle, capi, monkeypatch, be):
     """F110QP_LANE_KMAX=1 lets no QP with an active bound settle in the lane kernel: those go
     through the device-side list to the wave kernel (GI). Results stay exact, and a second call
     on the same context reuses the other list counter."""
     monkeypatch.setenv("F110QP_LANE_KMAX", "1")
     N = 20
     w = workload.make_batch(3000, N, seed=991, heading="true", lateral=1.5, steer_range=1.0)
-    s = capi.Solver(capi.default_config(N, backend=capi.BACKEND_LANE))
+    s = capi.Solver(capi.default_config(N, backend=_be(capi, be)))
     ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"])
     for _ in range(3):
         u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
@@ -401,7 +412,7 @@ def test_lane_backend_hands_over_to_wave_kernel(oracle, capi, monkeypatch):
 
 
 def test_lane_and_wave_backends_agree(capi):
-    N, B = 20, 4096
+    N, B = 20, 4100
     w = workload.make_batch(B, N, seed=1234, heading="true", lateral=1.0)
     res = []
     for be in (capi.BACKEND_WAVE, capi.BACKEND_LANE, capi.BACKEND_AUTO):
@@ -414,11 +425,12 @@ def test_lane_and_wave_backends_agree(capi):
         assert rel_err(r[1], res[0][1].astype(np.float64)).max() <= 1e-5
 
 
-def test_lane_backend_warm_stream(oracle, capi):
+@pytest.mark.parametrize("be", RICCATI)
+def test_lane_backend_warm_stream(oracle, capi, be):
     """Config C5 on the lane back end: the previous tick's active set seeds PDAS."""
     N, B, T = 20, 4096, 5
     stream = workload.make_stream(B, N, T, seed=31, heading_change_every=2)
-    warm = capi.Solver(capi.default_config(N, warm_start=1, backend=capi.BACKEND_LANE))
+    warm = capi.Solver(capi.default_config(N, warm_start=1, backend=_be(capi, be)))
     its = []
     for t, w in enumerate(stream):
         u, x, st, it = warm.solve(w["x0"], w["u_lin"], w["x_ref"])
@@ -430,12 +442,13 @@ def test_lane_backend_warm_stream(oracle, capi):
     warm.close()
 
 
-def test_lane_backend_c4_shard(oracle, capi):
-    """BASELINE configs[3] at N = 40 through the lane back end (auto-selected at this size)."""
+@pytest.mark.parametrize("be", RICCATI + ["auto"])
+def test_lane_backend_c4_shard(oracle, capi, be):
+    """BASELINE configs[3] at N = 40 through the Riccati back ends (and whatever auto picks)."""
     N, B = 40, 8192
     g = workload.make_grouped_batch(69, N, seed=4041)
     w = {k: np.ascontiguousarray(g[k][:B]) for k in ("x0", "u_lin", "x_ref")}
-    s = capi.Solver(capi.default_config(N))
+    s = capi.Solver(capi.default_config(N, backend=capi.BACKEND_AUTO if be == "auto" else _be(capi, be)))
     u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
     s.close()
     assert (st == capi.SOLVED).all()
