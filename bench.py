@@ -44,13 +44,17 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
 
 
-def bytes_per_qp(N: int, gap: bool, warm: bool = False) -> int:
-    """ABI bytes moved per QP: x0, u_lin, x_ref (+ halfspace) in; u*, x*, status, iters out;
-    warm start adds the slot key and active masks (read + write) and one read of the cached
-    W = H^-1 (2N x 2N fp32) on a key hit."""
+def bytes_per_qp(N: int, gap: bool, warm: bool = False, backend: str = "wave") -> int:
+    """ABI bytes moved per QP: x0, u_lin, x_ref (+ halfspace) in; u*, x*, status, iters out.
+    Warm start adds the active masks (read + write; 2 x 64-bit words per 64 variables and side)
+    and, for the wave back end, the slot key and one read of the cached W = H^-1 (2N x 2N fp32)
+    on a key hit. Scratch traffic of the lane back end is not algorithmic (see "traffic")."""
     inp = 4 * (3 + 2 + 3 * N + (6 if gap else 0))
     out = 4 * (2 * N + 3 * (N + 1) + 1 + 1)
-    extra = (2 * 32 + 4 * (2 * N) ** 2) if warm else 0
+    rows = (2 * N + 63) // 64
+    extra = 0
+    if warm:
+        extra = 2 * 2 * 8 * rows + ((16 + 4 * (2 * N) ** 2) if backend == "wave" else 0)
     return inp + out + extra
 
 
@@ -186,6 +190,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the latency probes (profiling runs: only the config's launches)")
     ap.add_argument("--backend", default="auto", choices=["auto", "wave", "lane"],
                     help="solver back end (auto: lane-per-QP for box-only batches >= 2048)")
     args = ap.parse_args()
@@ -295,7 +301,7 @@ def main():
     # and through the host-pointer entry point (H2D + launch + D2H), plus the per-launch
     # distribution of the configured batch; rank 0 only, outside the timed region
     latency = None
-    if rank == 0:
+    if rank == 0 and not args.no_latency:
         latency = measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step)
 
     if strong:
@@ -307,7 +313,7 @@ def main():
         total_qps = Bper * world * args.steps
     value = total_qps / el
     ms_per_step = el / args.steps * 1e3
-    bpq = bytes_per_qp(N, gap, warm)
+    bpq = bytes_per_qp(N, gap, warm, be_name)
     # active-set size ~ iterations for an add-only run; use iterations as the upper bound
     fpq = flops_per_qp(N, float(itn.mean()), float(itn.mean()))
     achieved_gbs = bpq * Bper / (kms * 1e-3) / 1e9

@@ -130,10 +130,10 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     const int v = std::atoi(ek);
     if (v >= 1 && v <= 64) c->lane_kmax = v;
   }
-  // test/bench hook: F110QP_LANE_MODE = 1 LDS fp64, 2 LDS fp32, 3 HBM fp64 scratch
+  // test/bench hook: F110QP_LANE_MODE = 1 LDS fp64, 2 LDS fp32, 3 HBM fp64, 4 HBM fp32 scratch
   if (const char* em = std::getenv("F110QP_LANE_MODE")) {
     const int v = std::atoi(em);
-    if (v >= 0 && v <= 3) c->lane_mode = v;
+    if (v >= 0 && v <= 4) c->lane_mode = v;
   }
   const int nu = 2 * cfg->horizon;
   k.max_iter = cfg->max_iter > 0 ? cfg->max_iter : 8 * (nu + (cfg->gap_mode ? nu : 0)) + 16;

@@ -44,7 +44,7 @@ struct LaneWork {
   int* fail_count = nullptr;
   int* fail_count_next = nullptr;
   int kmax = 16;  // PDAS passes before a QP is handed over
-  int mode = 0;   // scratch: 0 auto, 1 LDS fp64, 2 LDS fp32, 3 HBM fp64 (the workspace above)
+  int mode = 0;   // scratch: 0 auto, 1 LDS fp64, 2 LDS fp32, 3 HBM fp64, 4 HBM fp32 (workspace)
 };
 
 enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };

@@ -455,3 +455,15 @@ def test_lane_backend_c4_shard(oracle, capi, be):
     idx = np.concatenate([np.arange(0, B, 29), np.arange(480, 720)])
     ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
     assert rel_err(u[idx], ur).max() <= TOL and rel_err(x[idx], xr).max() <= TOL
+
+
+@pytest.mark.parametrize("mode", ["1", "2", "3", "4"])
+def test_lane_backend_scratch_modes(oracle, capi, monkeypatch, mode):
+    """Every Riccati-scratch placement of the lane back end (LDS fp64 / LDS fp32 / HBM fp64 /
+    HBM fp32, F110QP_LANE_MODE) gives the exact optimum within the tolerance; N = 40 covers
+    the fall-back of LDS fp64 (too big) to HBM."""
+    monkeypatch.setenv("F110QP_LANE_MODE", mode)
+    for N, seed in ((20, 811), (40, 812)):
+        w = workload.make_batch(1500, N, seed=seed, heading="true", lateral=1.2, steer_range=0.8)
+        u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE, tol=2e-6)
+        assert (st == capi.SOLVED).all()
