@@ -42,6 +42,9 @@ GROUP = 120  # candidates per scenario in c4 (6 lane offsets x 20 steer values)
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
+FP64_PEAK_TFLOPS = 78.6     # MI355X spec FP64 vector; tools/microbench/latency.hip measures the
+                            # matching issue rate (one wave64 fp64 FMA per 4 cycles per SIMD)
+LANE_FLOPS_PER_STAGE = 290  # fp64 flops per stage and pass of lane_kernel (ISA count)
 
 
 def bytes_per_qp(N: int, gap: bool, warm: bool = False, backend: str = "wave") -> int:
@@ -69,14 +72,16 @@ def flops_per_qp(N: int, mean_iters: float, mean_active: float) -> float:
         + 2 * (2 * n * n + 2 * q * q + 2 * n * q)
 
 
-def load_traffic(config: str):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if present."""
+def load_traffic(config: str, kernel: str):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary of this config, if it was
+    taken on the same kernel (tools/profile_round.sh + tools/summarize_profiles.py)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch") if kernel in d.get("kernel", "") else None
     except Exception:
         return None
 
@@ -315,10 +320,16 @@ def main():
     ms_per_step = el / args.steps * 1e3
     bpq = bytes_per_qp(N, gap, warm, be_name)
     # active-set size ~ iterations for an add-only run; use iterations as the upper bound
-    fpq = flops_per_qp(N, float(itn.mean()), float(itn.mean()))
+    if be_name == "lane":
+        # Riccati + forward + adjoint sweeps: (active-set changes + 1) passes over N stages
+        fpq = LANE_FLOPS_PER_STAGE * N * (float(itn.mean()) + 1.0)
+        cpeak, cname = FP64_PEAK_TFLOPS, "fp64_compute"
+    else:
+        fpq = flops_per_qp(N, float(itn.mean()), float(itn.mean()))
+        cpeak, cname = FP32_PEAK_TFLOPS, "fp32_compute"
     achieved_gbs = bpq * Bper / (kms * 1e-3) / 1e9
     achieved_tf = fpq * Bper / (kms * 1e-3) / 1e12
-    traffic = load_traffic(args.config)
+    traffic = load_traffic(args.config, "lane_kernel" if be_name == "lane" else "solve_kernel")
 
     out = {
         "metric": f"QP solves/s (horizon={N}, nx=3 reference model, nu=2)",
@@ -358,9 +369,12 @@ def main():
                        "lane": "f110qp::lane_kernel (+ solve_kernel hand-over launch)"}[be_name],
             "kernel_ms_per_launch": kms,
             "algorithmic_bytes_per_qp": bpq,
-            "fp32_compute": {"achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                             "frac": achieved_tf / FP32_PEAK_TFLOPS, "flops_per_qp": fpq},
-            "note": "latency-bound (serial active-set chain per wave); neither HBM nor FP32 peak binds",
+            cname: {"achieved": achieved_tf, "peak": cpeak, "unit": "TFLOP/s",
+                    "frac": achieved_tf / cpeak, "flops_per_qp": fpq},
+            "note": ("lane kernel: fp64 VALU-issue and scratch-latency bound (Riccati sweeps, 64 QPs per "
+                     "wave); traffic = PMC HBM bytes incl. the Riccati scratch" if be_name == "lane" else
+                     "wave kernel: latency-bound (serial active-set chain per wave); neither HBM nor FP32 "
+                     "peak binds"),
         },
     }
     if latency is not None:
