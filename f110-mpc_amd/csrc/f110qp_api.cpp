@@ -12,6 +12,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "f110qp.h"
 #include "f110qp_kernels.h"
@@ -363,6 +364,125 @@ int f110qp_find_half_spaces_dev(int batch, const float* states, const float* ran
                                             angle_max, ftg_thresh, divider, buffer, hs, gap_lo,
                                             gap_hi, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "half-space kernel launch");
+  return F110QP_OK;
+}
+
+// ---- planning stage -----------------------------------------------------------------------
+
+void f110qp_default_plan_config(f110qp_plan_config* c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof(*c));
+  c->size = 10;            // params.yaml:16
+  c->discrete = 0.1f;      // params.yaml:17
+  c->dilation = 0.15f;     // params.yaml:18
+  c->lookahead = 2.5f;     // params.yaml:63
+  c->speed_max = 4.5;      // params.yaml:46 (umax)
+  c->steer_max = 0.4;      // params.yaml:60
+  c->steer_discrete = 30;  // params.yaml:59
+  c->traj_discrete = 50;   // params.yaml:61
+  c->dt = 0.01;            // params.yaml:13
+}
+
+static int validate_plan(const f110qp_plan_config* c, int* G) {
+  if (!c) return fail(F110QP_ERR_INVALID, "plan config is NULL");
+  if (!(c->discrete > 0.f) || c->size <= 0 || !(c->dilation >= 0.f))
+    return fail(F110QP_ERR_INVALID, "occupancy grid size/discrete/dilation");
+  const int g = (int)((float)c->size / c->discrete);  // occupancy_grid.cpp:9
+  if (g < 1 || g > 200) return fail(F110QP_ERR_INVALID, "grid_blocks must be in [1, 200]");
+  if (c->steer_discrete < 1 || c->steer_discrete > 255 || c->traj_discrete < 2 || c->traj_discrete > 1024)
+    return fail(F110QP_ERR_INVALID, "steer_discrete in [1, 255], traj_discrete in [2, 1024]");
+  *G = g;
+  return F110QP_OK;
+}
+
+// Traj_Plan::generate_traj_table (trajectory_planner.cpp:26-72) with Model::simulate_dynamics
+// (model.cpp:61-75, CAR_LENGTH = 0.35), doubles as the reference's State/Input.
+int f110qp_traj_table(const f110qp_plan_config* c, double* table) {
+  int G;
+  int rc = validate_plan(c, &G);
+  if (rc) return rc;
+  if (!table) return fail(F110QP_ERR_INVALID, "table is NULL");
+  const double ds = 2 * +c->steer_max / c->steer_discrete;  // :31
+  const int T = c->steer_discrete + 1, P = c->traj_discrete;
+  const double CAR_LENGTH = 0.35;
+  for (int i = 0; i < T; i++) {
+    const double steer = -c->steer_max + i * ds;  // :43
+    const double v = c->speed_max;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    double* row = table + (size_t)i * P * 3;
+    row[0] = s0; row[1] = s1; row[2] = s2;  // k == 0 (:54)
+    for (int k = 1; k < P; k++) {
+      const volatile double d0 = v * std::cos(s2), d1 = v * std::sin(s2);
+      const volatile double d2 = std::tan(steer) * v / CAR_LENGTH;
+      const volatile double e0 = d0 * c->dt, e1 = d1 * c->dt, e2 = d2 * c->dt;  // dynamics*dt
+      s0 = s0 + e0; s1 = s1 + e1; s2 = s2 + e2;
+      row[3 * k] = s0; row[3 * k + 1] = s1; row[3 * k + 2] = s2;
+    }
+  }
+  return T;
+}
+
+// Trajectory::ReadCSV (trajectory.cpp:18-55): getline(',') then getline() and stof of each.
+int f110qp_parse_waypoints(const char* text, double* wp, int max_n, int* n_out) {
+  if (!text || !wp || !n_out || max_n < 0) return fail(F110QP_ERR_INVALID, "NULL argument");
+  std::string buf;
+  int n = 0;
+  const char* s = text;
+  std::string xs, ys;
+  // temp.push_back(pair<float,float>(stof(coordX), stof(coordY)))
+  std::vector<float> tx, ty;
+  while (*s) {
+    const char* comma = std::strchr(s, ',');
+    if (!comma) break;
+    xs.assign(s, comma - s);
+    const char* eol = std::strchr(comma + 1, '\n');
+    ys.assign(comma + 1, eol ? (size_t)(eol - comma - 1) : std::strlen(comma + 1));
+    char* e1;
+    char* e2;
+    const float x = std::strtof(xs.c_str(), &e1);
+    const float y = std::strtof(ys.c_str(), &e2);
+    if (e1 == xs.c_str() || e2 == ys.c_str()) return fail(F110QP_ERR_INVALID, "stof: no conversion");
+    tx.push_back(x);
+    ty.push_back(y);
+    s = eol ? eol + 1 : comma + 1 + std::strlen(comma + 1);
+  }
+  const unsigned int cnt = (unsigned int)tx.size();
+  for (unsigned int i = 0; i < cnt && (int)i < max_n; i++) {
+    const unsigned int prev = (i - 1) % cnt;  // :42-43 (unsigned wrap for i = 0)
+    const float x = tx[i], y = ty[i];
+    wp[3 * i] = x;
+    wp[3 * i + 1] = y;
+    wp[3 * i + 2] = (float)std::atan2((double)(y - ty[prev]), (double)(x - tx[prev]));  // :46
+    n++;
+  }
+  *n_out = n;
+  return F110QP_OK;
+}
+
+int f110qp_plan_batch_dev(const f110qp_plan_config* c, int batch, const double* pose,
+                          const float* ranges, int nr, float angle_min, float angle_inc,
+                          float angle_max, const double* table, const double* wp, int W,
+                          unsigned char* grid, unsigned char* valid, int* best_global,
+                          int* best_traj, float* x_ref, float* x0, int* status, void* stream) {
+  int G;
+  int rc = validate_plan(c, &G);
+  if (rc) return rc;
+  if (batch < 0 || nr <= 0 || W < 0) return fail(F110QP_ERR_INVALID, "bad batch / num_ranges / num_waypoints");
+  if (batch == 0) return F110QP_OK;
+  if (!pose || !ranges || !table || (W > 0 && !wp) || !best_global || !best_traj || !x_ref || !x0 || !status)
+    return fail(F110QP_ERR_INVALID, "NULL pointer argument");
+  if (!(angle_inc > 0.f)) return fail(F110QP_ERR_INVALID, "angle_increment must be > 0");
+  f110qp::PlanKParams K;
+  K.G = G;
+  K.T = c->steer_discrete + 1;
+  K.P = c->traj_discrete;
+  K.discrete = c->discrete;
+  K.dilation = c->dilation;
+  K.lookahead = c->lookahead;
+  hipError_t e = f110qp::launch_plan(K, batch, pose, ranges, nr, angle_min, angle_inc, angle_max,
+                                     table, wp, W, grid, valid, best_global, best_traj, x_ref, x0,
+                                     status, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "plan kernel launch");
   return F110QP_OK;
 }
 

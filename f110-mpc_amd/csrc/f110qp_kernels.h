@@ -65,6 +65,22 @@ hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* u_
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* u_lin,
                                  const float* x_ref, double* H, double* g, hipStream_t stream);
 
+// Planning stage (plan_kernels.hip): grid size, candidate count / length, float params.
+struct PlanKParams {
+  int G;            // grid_blocks_ = size_ / discrete_
+  int T;            // candidates (steer_discrete + 1)
+  int P;            // points per candidate (traj_discrete)
+  float discrete;   // occ_discrete
+  float dilation;   // occ_dilation
+  float lookahead;  // Trajectory::lookahead
+};
+
+hipError_t launch_plan(const PlanKParams& K, int B, const double* pose, const float* ranges,
+                       int nr, float angle_min, float angle_inc, float angle_max,
+                       const double* table, const double* wp, int W, unsigned char* grid_out,
+                       unsigned char* valid_out, int* best_global, int* best_traj, float* x_ref,
+                       float* x0, int* status, hipStream_t stream);
+
 // Batched FindHalfSpaces (constraints.cpp:116-265), one wave per scan.
 hipError_t launch_half_spaces(int B, const float* states, const float* ranges, int num_ranges,
                               float angle_min, float angle_inc, float angle_max, float thresh,

@@ -51,6 +51,10 @@ EXPORTED = (
     "f110qp_warm_reset",
     "f110qp_find_half_spaces",
     "f110qp_find_half_spaces_dev",
+    "f110qp_default_plan_config",
+    "f110qp_traj_table",
+    "f110qp_parse_waypoints",
+    "f110qp_plan_batch_dev",
 )
 
 
@@ -68,6 +72,20 @@ class Config(C.Structure):
         ("device", C.c_int),
         ("warm_start", C.c_int),
         ("backend", C.c_int),
+    ]
+
+
+class PlanConfig(C.Structure):
+    _fields_ = [
+        ("size", C.c_int),
+        ("discrete", C.c_float),
+        ("dilation", C.c_float),
+        ("lookahead", C.c_float),
+        ("speed_max", C.c_double),
+        ("steer_max", C.c_double),
+        ("steer_discrete", C.c_int),
+        ("traj_discrete", C.c_int),
+        ("dt", C.c_double),
     ]
 
 
@@ -101,6 +119,11 @@ def load():
                                           C.c_float, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.f110qp_find_half_spaces_dev.argtypes = [C.c_int, fp, fp, C.c_int, C.c_float, C.c_float, C.c_float,
                                               C.c_float, C.c_float, C.c_float, fp, fp, fp, fp]
+    L.f110qp_default_plan_config.argtypes = [C.POINTER(PlanConfig)]
+    L.f110qp_traj_table.argtypes = [C.POINTER(PlanConfig), fp]
+    L.f110qp_parse_waypoints.argtypes = [C.c_char_p, fp, C.c_int, C.POINTER(C.c_int)]
+    L.f110qp_plan_batch_dev.argtypes = [C.POINTER(PlanConfig), C.c_int, fp, fp, C.c_int, C.c_float, C.c_float,
+                                        C.c_float, fp, fp, C.c_int, fp, fp, fp, fp, fp, fp, fp, fp]
     _lib = L
     return L
 
@@ -234,3 +257,51 @@ def find_half_spaces_dev(states, ranges, angle_min, angle_inc, angle_max, hs_out
                                          float(angle_max), float(thresh), float(divider), float(buffer),
                                          _tp(hs_out), _tp(gap_lo), _tp(gap_hi), C.c_void_p(stream.cuda_stream)),
            "f110qp_find_half_spaces_dev")
+
+
+# ---- planning stage (plan_kernels.hip) ---------------------------------------------------------
+
+def default_plan_config(**over) -> PlanConfig:
+    c = PlanConfig()
+    load().f110qp_default_plan_config(C.byref(c))
+    for k, v in over.items():
+        setattr(c, k, v)
+    return c
+
+
+def traj_table(cfg: PlanConfig) -> np.ndarray:
+    """Traj_Plan::generate_traj_table (host): [T, P, 3] float64, car frame."""
+    t = np.zeros((cfg.steer_discrete + 1, cfg.traj_discrete, 3), np.float64)
+    rc = load().f110qp_traj_table(C.byref(cfg), _p(t))
+    if rc < 0:
+        _check(rc, "f110qp_traj_table")
+    return t
+
+
+def parse_waypoints(text: str, max_n: int = 100000) -> np.ndarray:
+    """Trajectory::ReadCSV on CSV text: [n, 3] (x, y, ori)."""
+    wp = np.zeros((max_n, 3), np.float64)
+    n = C.c_int(0)
+    _check(load().f110qp_parse_waypoints(text.encode(), _p(wp), max_n, C.byref(n)), "f110qp_parse_waypoints")
+    return wp[: n.value].copy()
+
+
+def grid_blocks(cfg: PlanConfig) -> int:
+    return int(np.float32(cfg.size) / np.float32(cfg.discrete))
+
+
+def plan_batch_dev(cfg: PlanConfig, pose, ranges, angle_min, angle_inc, angle_max, table, waypoints, x_ref, x0,
+                   best_traj, best_global, status, valid=None, grid=None, stream=None):
+    """Batched planning stage on torch device tensors: pose [B,4] f64, ranges [B,R] f32, table
+    [T,P,3] f64, waypoints [W,2] f64 -> x_ref [B,P,3] f32, x0 [B,3] f32, best_traj / best_global
+    / status [B] i32 (valid [B,T] u8 and grid [B,G,G] u8 optional)."""
+    import torch
+
+    B = pose.shape[0]
+    if stream is None:
+        stream = torch.cuda.current_stream(pose.device)
+    _check(load().f110qp_plan_batch_dev(C.byref(cfg), B, _tp(pose), _tp(ranges), ranges.shape[1], float(angle_min),
+                                        float(angle_inc), float(angle_max), _tp(table), _tp(waypoints),
+                                        waypoints.shape[0], _tp(grid), _tp(valid), _tp(best_global), _tp(best_traj),
+                                        _tp(x_ref), _tp(x0), _tp(status), C.c_void_p(stream.cuda_stream)),
+           "f110qp_plan_batch_dev")

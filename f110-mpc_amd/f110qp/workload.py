@@ -131,3 +131,67 @@ def make_stream(batch: int, horizon: int, ticks: int, seed: int = 0, dt: float =
                 x0[turners, 2] += rng.uniform(-0.05, 0.05, int(turners.sum()))
         ticks_out.append(dict(x0=x0.astype(np.float32), u_lin=base["u_lin"].copy(), x_ref=base["x_ref"].copy()))
     return ticks_out
+
+
+# ---- planning scenes (pose + LaserScan + global path) for the device planning stage -----------
+
+def track_waypoints(n: int = 500, a: float = 12.0, b: float = 6.0) -> np.ndarray:
+    """A closed elliptical global path of n points (x, y as float32 values, like the CSV)."""
+    t = np.linspace(0.0, 2 * np.pi, n, endpoint=False)
+    return np.stack([a * np.cos(t), b * np.sin(t)], 1).astype(np.float32).astype(np.float64)
+
+
+def _ray_circles(ox, oy, ang, cx, cy, rad, max_range):
+    """Ray casting: ranges [B, R] from origins (ox, oy) [B] along angles [B, R] against circles
+    (cx, cy, rad) [B, C]."""
+    dx, dy = np.cos(ang), np.sin(ang)                       # [B, R]
+    px = cx[:, None, :] - ox[:, None, None]                 # [B, 1, C]
+    py = cy[:, None, :] - oy[:, None, None]
+    t = px * dx[..., None] + py * dy[..., None]             # projection, [B, R, C]
+    d2 = px * px + py * py - t * t
+    r2 = (rad * rad)[:, None, :]
+    hit = (d2 <= r2) & (t > 0)
+    th = t - np.sqrt(np.maximum(r2 - d2, 0.0))
+    th = np.where(hit & (th > 0), th, np.inf)
+    return np.minimum(th.min(axis=2), max_range)
+
+
+def make_scenes(batch: int, seed: int = 0, beams: int = SCAN_BEAMS, obstacles: int = 6, waypoints=None,
+                max_range: float = 10.0):
+    """Scenarios for project::OdomCallback's planning branch: a car near the global path with the
+    path heading (+ noise), its 1080-beam 2*pi LaserScan (from the lidar 0.275 m ahead, as
+    OccGrid::FillOccGrid assumes, occupancy_grid.cpp:63-64) of the two track walls (circles along
+    the path at +-1.6 m) and a few obstacles. Returns dict(pose [B,4] f64 (x, y, qz, qw),
+    ranges [B,beams] f32, geometry, waypoints [W,2] f64)."""
+    rng = np.random.default_rng(seed)
+    wp = track_waypoints() if waypoints is None else np.asarray(waypoints, np.float64)[:, :2]
+    W = wp.shape[0]
+    k = rng.integers(0, W, batch)
+    nxt = wp[(k + 1) % W]
+    hd = np.arctan2(nxt[:, 1] - wp[k, 1], nxt[:, 0] - wp[k, 0])
+    yaw = hd + rng.uniform(-0.3, 0.3, batch)
+    off = rng.uniform(-0.4, 0.4, batch)
+    x = wp[k, 0] - np.sin(hd) * off
+    y = wp[k, 1] + np.cos(hd) * off
+    pose = np.stack([x, y, np.sin(yaw / 2), np.cos(yaw / 2)], 1)
+    # walls: circles of radius 0.12 every ~0.25 m along the path, +-1.6 m laterally
+    hw = np.arctan2(np.roll(wp[:, 1], -1) - wp[:, 1], np.roll(wp[:, 0], -1) - wp[:, 0])
+    wall = np.concatenate([wp + 1.6 * np.stack([-np.sin(hw), np.cos(hw)], 1),
+                           wp - 1.6 * np.stack([-np.sin(hw), np.cos(hw)], 1)])
+    # only the wall circles within max_range of the car matter
+    amin, ainc, amax = scan_geometry(beams)
+    ang = yaw[:, None] + (amin + ainc * np.arange(beams, dtype=np.float64))[None, :]
+    lx, ly = x + 0.275 * np.cos(yaw), y + 0.275 * np.sin(yaw)
+    d = np.hypot(wall[None, :, 0] - lx[:, None], wall[None, :, 1] - ly[:, None])
+    near = np.argsort(d, axis=1)[:, :160]
+    cx = np.take_along_axis(np.broadcast_to(wall[:, 0], d.shape), near, 1)
+    cy = np.take_along_axis(np.broadcast_to(wall[:, 1], d.shape), near, 1)
+    rad = np.full(cx.shape, 0.12)
+    # obstacles 1-4 m ahead in a +-60 degree cone
+    ob_r = rng.uniform(1.0, 4.0, (batch, obstacles))
+    ob_a = yaw[:, None] + rng.uniform(-1.0, 1.0, (batch, obstacles))
+    cx = np.concatenate([cx, lx[:, None] + ob_r * np.cos(ob_a)], 1)
+    cy = np.concatenate([cy, ly[:, None] + ob_r * np.sin(ob_a)], 1)
+    rad = np.concatenate([rad, rng.uniform(0.1, 0.35, (batch, obstacles))], 1)
+    ranges = _ray_circles(lx, ly, ang, cx, cy, rad, max_range).astype(np.float32)
+    return dict(pose=pose, ranges=ranges, angle_min=amin, angle_inc=ainc, angle_max=amax, waypoints=wp)

@@ -142,6 +142,50 @@ int f110qp_find_half_spaces_dev(int batch, const float* states, const float* ran
                                 float angle_max, float ftg_thresh, float divider, float buffer,
                                 float* hs_out, int* gap_lo, int* gap_hi, void* stream);
 
+/* ---- planning stage in front of MPC::Update (src/project.cpp:73-152) ----------------------- */
+
+typedef struct {
+  int size;            /* occ_size, params.yaml:16 (OccGrid::size_ is int)                    */
+  float discrete;      /* occ_discrete, params.yaml:17 (float)                                  */
+  float dilation;      /* occ_dilation, params.yaml:18 (float)                                  */
+  float lookahead;     /* lookahead, params.yaml:63 (Trajectory::lookahead is float)            */
+  double speed_max;    /* umax as Traj_Plan reads it, params.yaml:46                            */
+  double steer_max;    /* steer_max, params.yaml:60                                             */
+  int steer_discrete;  /* params.yaml:59: T = steer_discrete + 1 candidates                     */
+  int traj_discrete;   /* params.yaml:61: P points per candidate                               */
+  double dt;           /* params.yaml:13 (Traj_Plan::dt is double)                              */
+} f110qp_plan_config;
+
+/* params.yaml defaults of the planning stage. */
+void f110qp_default_plan_config(f110qp_plan_config* cfg);
+
+/* Traj_Plan::generate_traj_table (src/trajectory_planner.cpp:26-72), host code: table
+ * [T][P][3] doubles (car frame). Returns T (> 0) or a negative error code. */
+int f110qp_traj_table(const f110qp_plan_config* cfg, double* table);
+
+/* Trajectory::ReadCSV (src/trajectory.cpp:18-55) on CSV text in memory: wp[n][3] = (x, y, ori)
+ * with the reference's float parsing and its (0u - 1) % n predecessor of point 0. Writes the
+ * count to *n; returns F110QP_OK or F110QP_ERR_INVALID. */
+int f110qp_parse_waypoints(const char* text, double* wp, int max_n, int* n);
+
+/* The planning branch of project::OdomCallback (src/project.cpp:73-152) for B scenarios on the
+ * device, one workgroup each: OccGrid::FillOccGrid of the scenario's LaserScan
+ * (src/occupancy_grid.cpp:55-88), the collision check of the T candidates, the lookahead
+ * waypoint (src/trajectory.cpp:81-126) and the nearest valid end point. Device pointers:
+ *   pose [B][4] doubles (x, y, qz, qw; planar odometry pose), ranges [B][num_ranges],
+ *   table [T][P][3] (f110qp_traj_table), waypoints [W][2] (x, y);
+ * outputs: x_ref [B][P][3] = the chosen candidate in the map frame with ori 0 (miniPath_,
+ * src/project.cpp:149-152; NaN without a candidate), x0 [B][3] = (x, y, GetCarOrientation)
+ * for f110qp_solve_batch_dev, best_traj / best_global [B], status [B] (0 ok, 1 no valid
+ * candidate — the reference returns before MPC, 2 no waypoint ahead — the reference throws);
+ * valid [B][T] and grid [B][G][G] (G = size / discrete) may be NULL. */
+int f110qp_plan_batch_dev(const f110qp_plan_config* cfg, int batch, const double* pose,
+                          const float* ranges, int num_ranges, float angle_min,
+                          float angle_increment, float angle_max, const double* table,
+                          const double* waypoints, int num_waypoints, unsigned char* grid,
+                          unsigned char* valid, int* best_global, int* best_traj, float* x_ref,
+                          float* x0, int* status, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

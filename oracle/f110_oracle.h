@@ -115,6 +115,42 @@ int f110o_admm_solve_batch(const f110o_params* prm, const f110o_admm_settings* s
                            const float* hs, int gap_active, double* u_out, int* status,
                            int* iters, int num_threads);
 
+/* ---- planning stage in front of MPC::Update (plan_oracle.c; project.cpp:64-152) ---------- */
+typedef struct {
+  int size;            /* occ_size (OccGrid::size_ int), params.yaml:16 */
+  float discrete;      /* occ_discrete (float), params.yaml:17 */
+  float dilation;      /* occ_dilation (float), params.yaml:18 */
+  float lookahead;     /* lookahead (Trajectory::lookahead float), params.yaml:63 */
+  double speed_max;    /* umax as read by Traj_Plan (double), params.yaml:46 */
+  double steer_max;    /* steer_max (double), params.yaml:60 */
+  int steer_discrete;  /* params.yaml:59 (T = steer_discrete + 1 candidates) */
+  int traj_discrete;   /* params.yaml:61 (P points per candidate) */
+  double dt;           /* params.yaml:13 (Traj_Plan::dt double) */
+} f110o_plan_params;
+
+void f110o_default_plan_params(f110o_plan_params* p);
+int f110o_grid_blocks(const f110o_plan_params* p);
+/* trajectory_planner.cpp:26-72: table[T][P][3] (car frame, double); returns T */
+int f110o_traj_table(const f110o_plan_params* p, double* table);
+/* transforms.cpp:44-47 for pose = (x, y, qz, qw) */
+float f110o_car_orientation(const double pose[4]);
+/* the float dilation offsets of occupancy_grid.cpp:77-78; returns their count */
+int f110o_dilation_offsets(const f110o_plan_params* p, float* offs, int max_n);
+/* occupancy_grid.cpp:55-88: grid[G][G] (row = y cell), occ_offset_ */
+void f110o_fill_occ_grid(const f110o_plan_params* p, const double pose[4], const float* ranges,
+                         int nr, float angle_min, float angle_inc, float angle_max,
+                         unsigned char* grid, float off[2]);
+/* project.cpp:73-152 + trajectory.cpp:81-126: valid[T], best waypoint / candidate, the chosen
+ * candidate in the map frame x_ref[P][3] (ori 0) and the MPC state x0. waypoints[W][2].
+ * Returns 0, 1 (no valid candidate: the reference returns before MPC) or 2 (no waypoint ahead:
+ * the reference throws on waypoints_.at(-1)). */
+int f110o_plan(const f110o_plan_params* p, const double pose[4], const unsigned char* grid,
+               const float off[2], const double* table, const double* waypoints, int W,
+               unsigned char* valid, int* best_global, int* best_traj, float* x_ref,
+               float x0[3]);
+/* trajectory.cpp:18-55 on CSV text: wp[n][3] = (x, y, ori); returns n */
+int f110o_parse_waypoints(const char* text, double* wp, int max_n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,6 +10,10 @@ Every function restates a reference routine (paths relative to the reference rep
   find_half_spaces      src/constraints.cpp:116-265
   assemble              src/mpc.cpp:26-29,208-340
   solve / solve_batch   OSQP's role at src/mpc.cpp:81-142, solved exactly (see f110_oracle.c)
+  traj_table            src/trajectory_planner.cpp:26-72
+  fill_occ_grid         src/occupancy_grid.cpp:55-88
+  plan                  src/project.cpp:73-152, src/trajectory.cpp:81-126
+  parse_waypoints       src/trajectory.cpp:18-55
 """
 from __future__ import annotations
 
@@ -37,6 +41,20 @@ class Params(C.Structure):
         ("u_des", C.c_double * 2),
         ("u_min", C.c_float * 2),
         ("u_max", C.c_float * 2),
+    ]
+
+
+class PlanParams(C.Structure):
+    _fields_ = [
+        ("size", C.c_int),
+        ("discrete", C.c_float),
+        ("dilation", C.c_float),
+        ("lookahead", C.c_float),
+        ("speed_max", C.c_double),
+        ("steer_max", C.c_double),
+        ("steer_discrete", C.c_int),
+        ("traj_discrete", C.c_int),
+        ("dt", C.c_double),
     ]
 
 
@@ -90,6 +108,17 @@ def lib():
                                            dp, C.c_int, dp, dp, ip]
             L.f110o_admm_solve_batch.argtypes = [C.POINTER(Params), C.POINTER(AdmmSettings), C.c_int,
                                                  fp, fp, fp, fp, C.c_int, dp, ip, ip, C.c_int]
+        pp = C.POINTER(PlanParams)
+        up = C.POINTER(C.c_ubyte)
+        L.f110o_default_plan_params.argtypes = [pp]
+        L.f110o_grid_blocks.argtypes = [pp]
+        L.f110o_traj_table.argtypes = [pp, dp]
+        L.f110o_car_orientation.argtypes = [dp]
+        L.f110o_car_orientation.restype = C.c_float
+        L.f110o_dilation_offsets.argtypes = [pp, fp, C.c_int]
+        L.f110o_fill_occ_grid.argtypes = [pp, dp, fp, C.c_int, C.c_float, C.c_float, C.c_float, up, fp]
+        L.f110o_plan.argtypes = [pp, dp, up, fp, dp, dp, C.c_int, up, ip, ip, fp, fp]
+        L.f110o_parse_waypoints.argtypes = [C.c_char_p, dp, C.c_int]
         for name in ("f110o_num_variables", "f110o_num_constraints", "f110o_nnz_P", "f110o_nnz_A"):
             getattr(L, name).argtypes = [C.c_int]
         _lib = L
@@ -242,3 +271,58 @@ def admm_solve_batch(prm: Params, settings: AdmmSettings, x0, u_lin, x_ref, hs=N
                                  _ptr(h, fp), int(gap_active), _ptr(u), _ptr(st, C.c_int), _ptr(it, C.c_int),
                                  int(num_threads))
     return u, st, it
+
+
+# ---- planning stage (plan_oracle.c) ------------------------------------------------------------
+
+def plan_params(**over) -> PlanParams:
+    p = PlanParams()
+    lib().f110o_default_plan_params(C.byref(p))
+    for k, v in over.items():
+        setattr(p, k, v)
+    return p
+
+
+def traj_table(pp: PlanParams) -> np.ndarray:
+    T, P = pp.steer_discrete + 1, pp.traj_discrete
+    t = np.zeros((T, P, 3), np.float64)
+    lib().f110o_traj_table(C.byref(pp), _ptr(t))
+    return t
+
+
+def dilation_offsets(pp: PlanParams) -> np.ndarray:
+    buf = np.zeros(64, np.float32)
+    n = lib().f110o_dilation_offsets(C.byref(pp), _ptr(buf, C.c_float), 64)
+    return buf[:n].copy()
+
+
+def fill_occ_grid(pp: PlanParams, pose, ranges, angle_min, angle_inc, angle_max):
+    """pose = (x, y, qz, qw) doubles -> (grid [G, G] uint8, occ_offset [2] float32)"""
+    G = lib().f110o_grid_blocks(C.byref(pp))
+    grid = np.zeros((G, G), np.uint8)
+    off = np.zeros(2, np.float32)
+    r = np.ascontiguousarray(ranges, np.float32)
+    lib().f110o_fill_occ_grid(C.byref(pp), _ptr(_d(pose)), _ptr(r, C.c_float), r.shape[0], angle_min,
+                              angle_inc, angle_max, _ptr(grid, C.c_ubyte), _ptr(off, C.c_float))
+    return grid, off
+
+
+def plan(pp: PlanParams, pose, grid, off, table, waypoints):
+    """-> dict(status, valid [T] uint8, best_global, best_traj, x_ref [P, 3] f32, x0 [3] f32)"""
+    T, P = pp.steer_discrete + 1, pp.traj_discrete
+    wp = _d(np.asarray(waypoints)[:, :2])
+    valid = np.zeros(T, np.uint8)
+    bg, bt = C.c_int(-1), C.c_int(-1)
+    xr = np.zeros((P, 3), np.float32)
+    x0 = np.zeros(3, np.float32)
+    st = lib().f110o_plan(C.byref(pp), _ptr(_d(pose)), _ptr(np.ascontiguousarray(grid, np.uint8), C.c_ubyte),
+                          _ptr(np.ascontiguousarray(off, np.float32), C.c_float), _ptr(_d(table)), _ptr(wp),
+                          wp.shape[0], _ptr(valid, C.c_ubyte), C.byref(bg), C.byref(bt), _ptr(xr, C.c_float),
+                          _ptr(x0, C.c_float))
+    return dict(status=st, valid=valid, best_global=bg.value, best_traj=bt.value, x_ref=xr, x0=x0)
+
+
+def parse_waypoints(text: str, max_n: int = 100000) -> np.ndarray:
+    wp = np.zeros((max_n, 3), np.float64)
+    n = lib().f110o_parse_waypoints(text.encode(), _ptr(wp), max_n)
+    return wp[:n].copy()
