@@ -38,6 +38,10 @@ CONFIGS = {
                                     "candidate sets (grouped), sharded over the GPUs"),
 }
 STRONG = {"c4"}
+# the whole control tick on the device: planning stage (occupancy grid, collision check of the 31
+# candidates, lookahead waypoint, selection; project.cpp:73-152) then the QP of every scenario
+CONFIGS["tick"] = (1024, 20, False, False, "control tick x1024 scenarios: device planning stage (1080-beam "
+                   "scan -> 100x100 occupancy grid -> 31 candidates -> lookahead waypoint -> x_ref) + QP, N=20")
 GROUP = 120  # candidates per scenario in c4 (6 lane offsets x 20 steer values)
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -146,6 +150,7 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
     st = torch.empty((1,), dtype=torch.int32, device=dev)
     c1 = type(cfg).from_buffer_copy(cfg)
     c1.warm_start = 0  # a cold solve per call: the latency of one control tick
+    c1.x_ref_points = 0
     s1 = capi.Solver(c1)
     dev_t, host_t, batch_t = [], [], []
     for i in range(reps + 20):
@@ -220,6 +225,22 @@ def main():
         Bper = args.batch
     strong = args.config in STRONG
     stream_cfg = args.config.startswith("c5")
+    tick_cfg = args.config == "tick"
+    if tick_cfg:
+        sc = workload.make_scenes(Bper, seed=3000 + rank)
+        pcfg = capi.default_plan_config()
+        ptab = torch.from_numpy(capi.traj_table(pcfg)).to(dev)
+        ppose = torch.from_numpy(sc["pose"]).to(dev)
+        pranges = torch.from_numpy(sc["ranges"]).to(dev)
+        pwp = torch.from_numpy(np.ascontiguousarray(sc["waypoints"][:, :2])).to(dev)
+        P = pcfg.traj_discrete
+        pxr = torch.empty((Bper, P, 3), dtype=torch.float32, device=dev)
+        px0 = torch.empty((Bper, 3), dtype=torch.float32, device=dev)
+        pbt = torch.empty(Bper, dtype=torch.int32, device=dev)
+        pbg = torch.empty(Bper, dtype=torch.int32, device=dev)
+        pst = torch.empty(Bper, dtype=torch.int32, device=dev)
+        w = workload.make_batch(Bper, N, seed=1000 + rank)  # u_lin (v = 4.5, project.cpp:170)
+        w["u_lin"][:, 1] = 0.0
     if strong:
         # one global batch of grouped candidates; this rank solves its scenario-aligned shard
         from f110qp import shard
@@ -252,15 +273,25 @@ def main():
     it = torch.empty((Bper,), dtype=torch.int32, device=dev)
     backend = {"auto": capi.BACKEND_AUTO, "wave": capi.BACKEND_WAVE, "lane": capi.BACKEND_LANE}[args.backend]
     cfg = capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, device=dev.index,
-                              warm_start=int(warm), backend=backend)
+                              warm_start=int(warm), backend=backend,
+                              x_ref_points=(pcfg.traj_discrete if tick_cfg else 0))
     eff = capi.auto_backend(N, Bper, gap) if backend == capi.BACKEND_AUTO else backend
     be_name = "lane" if (eff == capi.BACKEND_LANE and not gap) else "wave"
     solver = capi.Solver(cfg)
     stream = torch.cuda.current_stream(dev)
     tick = [0]
 
+    def plan_step():
+        capi.plan_batch_dev(pcfg, ppose, pranges, sc["angle_min"], sc["angle_inc"], sc["angle_max"], ptab, pwp,
+                            pxr, px0, pbt, pbg, pst, stream=stream)
+
     def step():
-        if stream_cfg:
+        if tick_cfg:
+            plan_step()
+            # scenarios without a valid candidate keep NaN x_ref and come back non-solved,
+            # as MPC::Update is skipped for them in the reference (project.cpp:117-121)
+            solver.solve_dev(px0, ul, pxr, hs, uo, xo, st, it, stream=stream)
+        elif stream_cfg:
             t = tick[0] % X0.shape[0]  # the latency probe after the timed region wraps around
             tick[0] += 1
             solver.solve_dev(X0[t], UL[t], XR[t], hs, uo, xo, st, it, stream=stream)
@@ -301,6 +332,19 @@ def main():
         evs.append((a, b))
     torch.cuda.synchronize(dev)
     kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))  # ms per launch
+    plan_ms = None
+    if tick_cfg:  # the planning kernel alone, same stream
+        pev = []
+        for _ in range(20):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            plan_step()
+            b.record(stream)
+            pev.append((a, b))
+        torch.cuda.synchronize(dev)
+        plan_ms = float(np.mean([a.elapsed_time(b) for a, b in pev]))
+        kms = kms - plan_ms  # the QP kernel(s) of the step
 
     # per-QP latency: single-QP solves (B = 1) through the device entry point (launch + sync)
     # and through the host-pointer entry point (H2D + launch + D2H), plus the per-launch
@@ -355,6 +399,8 @@ def main():
             "parallelism": f"independent QP shards x{world} (no collective)"
                            + (f", scenario-aligned ({GROUP}) split of one global batch" if strong else ""),
             "solved_fraction": solved,
+            **({"plan_kernel_ms": plan_ms, "planned_fraction": float((pst.cpu().numpy() == 0).mean()),
+                "step": "f110qp_plan_batch_dev + f110qp_solve_batch_dev (x_ref_points = 50)"} if tick_cfg else {}),
             "mean_active_set_iters": float(itn.mean()),
             "max_active_set_iters": int(itn.max()),
         },

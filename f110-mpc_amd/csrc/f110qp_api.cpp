@@ -86,6 +86,7 @@ void f110qp_default_config(f110qp_config* c, int horizon) {
   c->device = 0;
   c->warm_start = 0;
   c->backend = F110QP_BACKEND_AUTO;
+  c->x_ref_points = 0;
 }
 
 static int validate_config(const f110qp_config* c) {
@@ -103,6 +104,8 @@ static int validate_config(const f110qp_config* c) {
     return fail(F110QP_ERR_INVALID, "gap_mode must be F110QP_GAP_INACTIVE or F110QP_GAP_ACTIVE");
   if (c->max_iter < 0) return fail(F110QP_ERR_INVALID, "max_iter must be >= 0");
   if (c->warm_start != 0 && c->warm_start != 1) return fail(F110QP_ERR_INVALID, "warm_start must be 0 or 1");
+  if (c->x_ref_points != 0 && c->x_ref_points < c->horizon)
+    return fail(F110QP_ERR_INVALID, "x_ref_points must be 0 (= horizon) or >= horizon");
   if (c->backend < F110QP_BACKEND_AUTO || c->backend > F110QP_BACKEND_LANE)
     return fail(F110QP_ERR_INVALID, "backend must be F110QP_BACKEND_AUTO, _WAVE or _LANE");
   return F110QP_OK;
@@ -138,6 +141,7 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
   }
   const int nu = 2 * cfg->horizon;
   k.max_iter = cfg->max_iter > 0 ? cfg->max_iter : 8 * (nu + (cfg->gap_mode ? nu : 0)) + 16;
+  k.xr_stride = cfg->x_ref_points > 0 ? cfg->x_ref_points : cfg->horizon;
   *out = c;
   return F110QP_OK;
 }
@@ -259,7 +263,8 @@ int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* u
   const int N = c->cfg.horizon;
   const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
   const size_t B = (size_t)batch;
-  const size_t s_x0 = B * 3 * 4, s_ul = B * 2 * 4, s_xr = B * N * 3 * 4, s_hs = B * 6 * 4;
+  const size_t S = (size_t)c->kp.xr_stride;
+  const size_t s_x0 = B * 3 * 4, s_ul = B * 2 * 4, s_xr = B * S * 3 * 4, s_hs = B * 6 * 4;
   const size_t s_uo = B * N * 2 * 4, s_xo = B * (N + 1) * 3 * 4, s_st = B * 4;
   if ((e = c->x0.ensure(s_x0)) || (e = c->ul.ensure(s_ul)) || (e = c->xr.ensure(s_xr)) ||
       (gap && (e = c->hs.ensure(s_hs))) || (e = c->uo.ensure(s_uo)) || (e = c->xo.ensure(s_xo)) ||

@@ -21,6 +21,7 @@ struct KParams {
   float umin[2];  // input lower bounds
   float umax[2];  // input upper bounds
   int max_iter;   // active-set iteration cap
+  int xr_stride;  // points per QP in x_ref (>= N; the reference passes its whole miniPath)
 };
 
 // Warm-start state of a context (all null = cold solve). Per QP slot b of the batch:

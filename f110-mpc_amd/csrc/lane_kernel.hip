@@ -75,28 +75,31 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
   const int n3 = 3 * N;
   if (blockIdx.x == 0 && lane == 0) *fail_count_next = 0;  // the next call's list (double buffer)
 
-  // ---- stage the wave's reference paths (one contiguous block of nq * 3N floats) ----------
-  // Linear, coalesced sweep over the block (element e -> QP e / 3N, entry e % 3N), eight
-  // independent loads in flight per lane, written transposed to LDS.
+  // ---- stage the wave's reference paths (nq rows of 3S floats, the first 3N of each used) ---
+  // Linear, coalesced sweep over the rows' first 3N entries (element e -> QP e / 3N, entry
+  // e % 3N), eight independent loads in flight per lane, written transposed to LDS.
   {
+    const int S3 = 3 * P.xr_stride;  // floats per QP in x_ref (>= 3N)
     const int nq = (B - b0) < 64 ? (B - b0) : 64;
     const int tot = nq * n3;
-    const float* src = xrg + (size_t)b0 * n3;
+    const float* src = xrg + (size_t)b0 * S3;
     const float rn3 = 1.0f / (float)n3;
     for (int e0 = 0; e0 < tot; e0 += 8 * 64) {
       float vbuf[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int e = e0 + j * 64 + lane;
-        vbuf[j] = (e < tot) ? src[e] : 0.f;
-      }
+      int qv[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const int e = e0 + j * 64 + lane;
         int q = (int)((float)e * rn3);
         q -= (q * n3 > e) ? 1 : 0;
         q += ((q + 1) * n3 <= e) ? 1 : 0;
-        if (e < tot) xr_s[(e - q * n3) * 64 + q] = vbuf[j];
+        qv[j] = q;
+        vbuf[j] = (e < tot) ? src[(size_t)q * S3 + (e - q * n3)] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int e = e0 + j * 64 + lane;
+        if (e < tot) xr_s[(e - qv[j] * n3) * 64 + qv[j]] = vbuf[j];
       }
     }
     __syncthreads();
@@ -174,6 +177,22 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
   // the KKT conditions and the stored forward sweep is the solution.
   bool done = !live;
   double xN0 = 0.0, xN1 = 0.0, xN2 = 0.0;  // x_N of the last forward sweep
+  if (live) {
+    // non-finite data -> F110QP_NUMERICAL with NaN outputs (e.g. the planning stage's NaN x_ref
+    // of a scenario without a valid candidate, where the reference skips MPC::Update)
+    bool bad = !(isfinite(X0) && isfinite(Y0) && isfinite(th0) && isfinite(v) && isfinite(d));
+    for (int e = 0; e < n3; e++) bad = bad || !isfinite(xr_s[e * 64 + lane]);
+    if (bad) {
+      const float nanv = __int_as_float(0x7fc00000);
+      float* uo = uout + (size_t)b * 2 * N;
+      float* xo = xout + (size_t)b * 3 * (N + 1);
+      for (int e = 0; e < 2 * N; e++) uo[e] = nanv;
+      for (int e = 0; e < 3 * (N + 1); e++) xo[e] = nanv;
+      status_out[b] = F110QP_NUMERICAL_ID;
+      if (iters_out) iters_out[b] = 0;
+      done = true;
+    }
+  }
 #ifdef F110QP_STAMPS
   t_setup = __builtin_amdgcn_s_memtime() - t_start;
 #endif

@@ -617,6 +617,14 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   // ---- 1. inputs + Model::Linearize ----------------------------------------------------
   const float fX0 = x0g[3 * b + 0], fY0 = x0g[3 * b + 1], fTH0 = x0g[3 * b + 2];
   const double X0 = (double)fX0, Y0 = (double)fY0;
+  // non-finite data -> F110QP_NUMERICAL with NaN outputs (e.g. the NaN x_ref the planning stage
+  // emits for a scenario without a valid candidate, where the reference skips MPC::Update)
+  bool bad = !(isfinite(fX0) && isfinite(fY0) && isfinite(fTH0) && isfinite(ulg[2 * b]) &&
+               isfinite(ulg[2 * b + 1]));
+  if (lane == 0) {
+    const float* x00 = xrg + (size_t)b * P.xr_stride * 3;
+    bad = bad || !(isfinite(x00[0]) && isfinite(x00[1]) && isfinite(x00[2]));
+  }
   {
     const Lin M = linearize((double)fTH0, (double)ulg[2 * b + 0], (double)ulg[2 * b + 1], P.dt);
     if (lane == 0) sm.M = M;
@@ -628,14 +636,16 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       float rth = 0.f;
       if (valid[r]) {
         const int ri = (kk[r] + 1 < N) ? kk[r] + 1 : N - 1;
-        const float* xr = xrg + ((size_t)b * N + ri) * 3;
+        const float* xr = xrg + ((size_t)b * P.xr_stride + ri) * 3;
         rx = (double)xr[0] - X0;
         ry = (double)xr[1] - Y0;
         rth = xr[2];
+        bad = bad || !(isfinite(xr[0]) && isfinite(xr[1]) && isfinite(xr[2]));
       }
       sm.rx[vv[r]] = rx; sm.ry[vv[r]] = ry; sm.rth[vv[r]] = rth;
     }
   }
+  const bool numerical = __ballot(bad) != 0ull;
   const float umin0 = P.umin[0], umin1 = P.umin[1], umax0 = P.umax[0], umax1 = P.umax[1];
   float lb[R], ub[R];
 #pragma unroll
@@ -828,7 +838,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   int q = 0;
   int it = 0;
   const int max_iter = P.max_iter;
-  int status = infeasible0 ? F110QP_PRIMAL_INFEASIBLE_ID : F110QP_SOLVED_ID;
+  int status = numerical ? F110QP_NUMERICAL_ID
+                         : (infeasible0 ? F110QP_PRIMAL_INFEASIBLE_ID : F110QP_SOLVED_ID);
   int reentries = 0;
   double u64[R];
 #pragma unroll

@@ -72,6 +72,7 @@ class Config(C.Structure):
         ("device", C.c_int),
         ("warm_start", C.c_int),
         ("backend", C.c_int),
+        ("x_ref_points", C.c_int),
     ]
 
 
@@ -191,7 +192,8 @@ class Solver:
         x0 = np.ascontiguousarray(x0, np.float32).reshape(-1, 3)
         B = x0.shape[0]
         ul = np.ascontiguousarray(u_lin, np.float32).reshape(B, 2)
-        xr = np.ascontiguousarray(x_ref, np.float32).reshape(B, N, 3)
+        S = self.config.x_ref_points or N
+        xr = np.ascontiguousarray(x_ref, np.float32).reshape(B, S, 3)
         hs = None if halfspace is None else np.ascontiguousarray(halfspace, np.float32).reshape(B, 6)
         u = np.empty((B, N, 2), np.float32)
         x = np.empty((B, N + 1, 3), np.float32)

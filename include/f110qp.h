@@ -25,8 +25,9 @@
  *  - Layouts (row-major, float32):
  *      x0        [B][3]      (x, y, ori)           State  (include/f110-mpc/state.h:10-45)
  *      u_lin     [B][2]      (v, steer_ang)        Input  (include/f110-mpc/input.h:11-34)
- *      x_ref     [B][N][3]   desired states 0..N-1 (the reference reads the first N of its
- *                            50-point mini path; stage N reuses x_ref[N-1], mpc.cpp:228)
+ *      x_ref     [B][S][3]   desired states, S = x_ref_points (default N); states 0..N-1 are
+ *                            read (the reference reads the first N of its 50-point mini path;
+ *                            stage N reuses x_ref[N-1], mpc.cpp:228)
  *      halfspace [B][2][3]   (l1, l2) = (a, b, c+0.5) from FindHalfSpaces, or NULL
  *      u_out     [B][N][2]   u*_k = z[3(N+1)+2k .. +1]            (mpc.cpp:148-157)
  *      x_out     [B][N+1][3] x*_k = z[3k .. 3k+2]                 (mpc.cpp:167-169)
@@ -41,7 +42,7 @@
 extern "C" {
 #endif
 
-#define F110QP_API_VERSION 2
+#define F110QP_API_VERSION 3
 
 /* return codes */
 #define F110QP_OK 0
@@ -89,6 +90,9 @@ typedef struct {
                     /*    previous call's, and the previous active set seeds the solve.    */
                     /*    Slot b of call t+1 continues slot b of call t (same batch size). */
   int backend;      /* F110QP_BACKEND_AUTO | _WAVE | _LANE (both give the exact optimum)    */
+  int x_ref_points; /* points per QP in x_ref, >= N (0 = N). MPC::Update receives the whole   */
+                    /* miniPath and reads its first N states (mpc.cpp:223-228): pass the      */
+                    /* planner's [B][P][3] x_ref with x_ref_points = P                        */
 } f110qp_config;
 
 /* Library / ABI version (F110QP_API_VERSION). */

@@ -30,7 +30,7 @@ def test_library_is_gfx950_code_object(capi):
 
 def test_version_and_defaults(capi):
     L = capi.load()
-    assert L.f110qp_version() == 2
+    assert L.f110qp_version() == 3
     c = capi.default_config(20)
     # params.yaml:1-13,42-47 and constraints.cpp:19,21
     assert c.horizon == 20 and c.dt == np.float32(0.01)
@@ -45,6 +45,7 @@ def test_version_and_defaults(capi):
     (dict(horizon=0), "horizon"),
     (dict(horizon=49), "horizon"),
     (dict(backend=3), "backend"),
+    (dict(x_ref_points=19), "x_ref_points"),
     (dict(r=[0.0, 5.0]), "R must be > 0"),
     (dict(q=[-1.0, 10.0, 0.0]), "Q must be"),
     (dict(u_min=[5.0, -0.43]), "u_min > u_max"),

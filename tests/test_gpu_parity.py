@@ -467,3 +467,26 @@ def test_lane_backend_scratch_modes(oracle, capi, monkeypatch, mode):
         w = workload.make_batch(1500, N, seed=seed, heading="true", lateral=1.2, steer_range=0.8)
         u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE, tol=2e-6)
         assert (st == capi.SOLVED).all()
+
+
+
+@pytest.mark.parametrize("be", ["wave", "lane"])
+def test_non_finite_inputs_are_numerical(oracle, capi, be):
+    """NaN / inf in x0, u_lin or x_ref (the planning stage emits a NaN x_ref when no candidate is
+    valid) -> status F110QP_NUMERICAL and NaN outputs for those QPs only; the rest exact."""
+    N, B = 20, 4160
+    w = workload.make_batch(B, N, seed=1313)
+    bad = {3: ("x_ref", (3, 5, 0), np.nan), 70: ("x0", (70, 2), np.inf), 130: ("u_lin", (130, 1), np.nan),
+           4000: ("x_ref", (4000, 0, 1), -np.inf), 4159: ("x_ref", (4159, N - 1, 2), np.nan)}
+    for b, (k, idx, v) in bad.items():
+        w[k][idx] = v
+    s = capi.Solver(capi.default_config(N, backend=_be(capi, be)))
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    badi = np.array(sorted(bad))
+    assert (st[badi] == capi.NUMERICAL).all()
+    assert np.isnan(u[badi]).all() and np.isnan(x[badi]).all()
+    good = np.setdiff1d(np.arange(B), badi)[::13]
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][good], w["u_lin"][good], w["x_ref"][good])
+    assert (st[good] == capi.SOLVED).all()
+    assert rel_err(u[good], ur).max() <= TOL and rel_err(x[good], xr).max() <= TOL

@@ -115,16 +115,19 @@ def test_tick_plan_then_qp_on_device(oracle, cuda):
     dev = run_plan_dev(cuda, cfg, sc, table, want_grid=False)
     ok = dev["status"] == 0
     x0 = torch.from_numpy(dev["x0"][ok]).to(cuda)
-    xr = torch.from_numpy(np.ascontiguousarray(dev["x_ref"][ok][:, :N])).to(cuda)
+    xr = torch.from_numpy(np.ascontiguousarray(dev["x_ref"][ok])).to(cuda)  # whole miniPath (P = 50)
     Bk = int(ok.sum())
     ul = torch.from_numpy(np.tile(np.float32([4.5, 0.0]), (Bk, 1))).to(cuda)  # set_v(4.5) (project.cpp:170)
     uo = torch.empty((Bk, N, 2), device=cuda)
     xo = torch.empty((Bk, N + 1, 3), device=cuda)
     st = torch.empty(Bk, dtype=torch.int32, device=cuda)
-    s = capi.Solver(capi.default_config(N))
-    s.solve_dev(x0, ul, xr, None, uo, xo, st)
-    torch.cuda.synchronize()
-    s.close()
+    outs = []
+    for be in (capi.BACKEND_WAVE, capi.BACKEND_LANE):  # x_ref_points = 50 on both back ends
+        s = capi.Solver(capi.default_config(N, x_ref_points=50, backend=be))
+        s.solve_dev(x0, ul, xr, None, uo, xo, st)
+        torch.cuda.synchronize()
+        s.close()
+        outs.append((uo.cpu().numpy().astype(np.float64), st.cpu().numpy()))
     x0r, xrr = [], []
     for b in np.nonzero(ok)[0]:
         g, off = oracle.fill_occ_grid(pp, sc["pose"][b], sc["ranges"][b], sc["angle_min"], sc["angle_inc"],
@@ -134,7 +137,7 @@ def test_tick_plan_then_qp_on_device(oracle, cuda):
         xrr.append(r["x_ref"][:N])
     ur, xref_r, sr = oracle.solve_batch(oracle.params(N), np.array(x0r), np.tile(np.float32([4.5, 0.0]), (Bk, 1)),
                                         np.array(xrr))
-    assert (st.cpu().numpy() == sr).all()
-    u = uo.cpu().numpy().astype(np.float64)
-    err = np.abs(u - ur).max(axis=(1, 2)) / np.maximum(1.0, np.abs(ur).max(axis=(1, 2)))
-    assert err.max() <= 1e-4
+    for u, stn in outs:
+        assert (stn == sr).all()
+        err = np.abs(u - ur).max(axis=(1, 2)) / np.maximum(1.0, np.abs(ur).max(axis=(1, 2)))
+        assert err.max() <= 1e-4
