@@ -200,6 +200,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse several "
+                         "ranks on fewer GPUs (ranks share devices round robin)")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the latency probes (profiling runs: only the config's launches)")
     ap.add_argument("--backend", default="auto", choices=["auto", "wave", "lane"],
@@ -212,11 +215,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+    gloo = args.dist_backend == "gloo"
+    ndev = max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", (local % ndev) if world > 1 else 0)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+
+    def allreduce(v: float, op) -> float:
+        """Scalar all-reduce over the ranks (RCCL on the device, or gloo on the host)."""
+        t = torch.tensor([v], dtype=torch.float64, device="cpu" if gloo else dev)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
 
     from f110qp import capi, workload
 
@@ -312,9 +325,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = allreduce(el, dist.ReduceOp.MAX)
 
     # solver statistics of the last step (all steps solve the same batch)
     stn = st.cpu().numpy()
@@ -354,10 +365,7 @@ def main():
         latency = measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step)
 
     if strong:
-        tq = torch.tensor([Bper], dtype=torch.int64, device=dev)
-        if world > 1:
-            dist.all_reduce(tq)
-        total_qps = int(tq.item()) * args.steps
+        total_qps = int(round(allreduce(float(Bper), dist.ReduceOp.SUM) if world > 1 else Bper)) * args.steps
     else:
         total_qps = Bper * world * args.steps
     value = total_qps / el
