@@ -30,8 +30,12 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(F110QP_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Device buffer that only grows.
+// Device buffer that only grows (freed with its owner).
 struct DevBuf {
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   void* p = nullptr;
   size_t bytes = 0;
   hipError_t ensure(size_t n) {
@@ -372,7 +376,13 @@ int f110qp_find_half_spaces_dev(int batch, const float* states, const float* ran
   return F110QP_OK;
 }
 
+}  // extern "C"
+
 // ---- planning stage -----------------------------------------------------------------------
+
+static int validate_plan(const f110qp_plan_config* c, int* G);
+
+extern "C" {
 
 void f110qp_default_plan_config(f110qp_plan_config* c) {
   if (!c) return;
@@ -492,3 +502,63 @@ int f110qp_plan_batch_dev(const f110qp_plan_config* c, int batch, const double* 
 }
 
 }  // extern "C"
+
+namespace {
+// device staging of f110qp_plan_batch, one set per host thread
+struct PlanBufs {
+  DevBuf pose, ranges, table, wp, grid, valid, bg, bt, xr, x0, st;
+  hipStream_t stream = nullptr;
+  ~PlanBufs() {
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+thread_local PlanBufs g_plan;
+}  // namespace
+
+extern "C" int f110qp_plan_batch(const f110qp_plan_config* c, int batch, const double* pose,
+                                 const float* ranges, int nr, float angle_min, float angle_inc,
+                                 float angle_max, const double* table, const double* wp, int W,
+                                 unsigned char* grid, unsigned char* valid, int* best_global,
+                                 int* best_traj, float* x_ref, float* x0, int* status) {
+  int G;
+  int rc = validate_plan(c, &G);
+  if (rc) return rc;
+  if (batch < 0 || nr <= 0 || W < 0) return fail(F110QP_ERR_INVALID, "bad batch / num_ranges / num_waypoints");
+  if (batch == 0) return F110QP_OK;
+  if (!pose || !ranges || !table || (W > 0 && !wp) || !best_global || !best_traj || !x_ref || !x0 || !status)
+    return fail(F110QP_ERR_INVALID, "NULL pointer argument");
+  PlanBufs& pb = g_plan;
+  hipError_t e;
+  if (!pb.stream && (e = hipStreamCreateWithFlags(&pb.stream, hipStreamNonBlocking)))
+    return hip_fail(e, "hipStreamCreate");
+  const size_t B = (size_t)batch, T = (size_t)c->steer_discrete + 1, P = (size_t)c->traj_discrete;
+  const size_t s_pose = B * 4 * 8, s_r = B * nr * 4, s_tab = T * P * 3 * 8, s_wp = (size_t)W * 2 * 8;
+  const size_t s_grid = B * G * G, s_valid = B * T, s_i = B * 4, s_xr = B * P * 3 * 4, s_x0 = B * 3 * 4;
+  if ((e = pb.pose.ensure(s_pose)) || (e = pb.ranges.ensure(s_r)) || (e = pb.table.ensure(s_tab)) ||
+      (e = pb.wp.ensure(s_wp ? s_wp : 8)) || (grid && (e = pb.grid.ensure(s_grid))) ||
+      (valid && (e = pb.valid.ensure(s_valid))) || (e = pb.bg.ensure(s_i)) || (e = pb.bt.ensure(s_i)) ||
+      (e = pb.xr.ensure(s_xr)) || (e = pb.x0.ensure(s_x0)) || (e = pb.st.ensure(s_i)))
+    return hip_fail(e, "hipMalloc plan workspace");
+  hipStream_t s = pb.stream;
+  if ((e = hipMemcpyAsync(pb.pose.p, pose, s_pose, hipMemcpyHostToDevice, s)) ||
+      (e = hipMemcpyAsync(pb.ranges.p, ranges, s_r, hipMemcpyHostToDevice, s)) ||
+      (e = hipMemcpyAsync(pb.table.p, table, s_tab, hipMemcpyHostToDevice, s)) ||
+      (W > 0 && (e = hipMemcpyAsync(pb.wp.p, wp, s_wp, hipMemcpyHostToDevice, s))))
+    return hip_fail(e, "hipMemcpyAsync H2D");
+  rc = f110qp_plan_batch_dev(c, batch, (const double*)pb.pose.p, (const float*)pb.ranges.p, nr, angle_min,
+                             angle_inc, angle_max, (const double*)pb.table.p, (const double*)pb.wp.p, W,
+                             grid ? (unsigned char*)pb.grid.p : nullptr,
+                             valid ? (unsigned char*)pb.valid.p : nullptr, (int*)pb.bg.p, (int*)pb.bt.p,
+                             (float*)pb.xr.p, (float*)pb.x0.p, (int*)pb.st.p, s);
+  if (rc) return rc;
+  if ((e = hipMemcpyAsync(best_global, pb.bg.p, s_i, hipMemcpyDeviceToHost, s)) ||
+      (e = hipMemcpyAsync(best_traj, pb.bt.p, s_i, hipMemcpyDeviceToHost, s)) ||
+      (e = hipMemcpyAsync(x_ref, pb.xr.p, s_xr, hipMemcpyDeviceToHost, s)) ||
+      (e = hipMemcpyAsync(x0, pb.x0.p, s_x0, hipMemcpyDeviceToHost, s)) ||
+      (e = hipMemcpyAsync(status, pb.st.p, s_i, hipMemcpyDeviceToHost, s)) ||
+      (grid && (e = hipMemcpyAsync(grid, pb.grid.p, s_grid, hipMemcpyDeviceToHost, s))) ||
+      (valid && (e = hipMemcpyAsync(valid, pb.valid.p, s_valid, hipMemcpyDeviceToHost, s))))
+    return hip_fail(e, "hipMemcpyAsync D2H");
+  if ((e = hipStreamSynchronize(s))) return hip_fail(e, "hipStreamSynchronize");
+  return F110QP_OK;
+}

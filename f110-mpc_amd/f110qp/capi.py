@@ -55,6 +55,7 @@ EXPORTED = (
     "f110qp_traj_table",
     "f110qp_parse_waypoints",
     "f110qp_plan_batch_dev",
+    "f110qp_plan_batch",
 )
 
 

@@ -195,3 +195,44 @@ def make_scenes(batch: int, seed: int = 0, beams: int = SCAN_BEAMS, obstacles: i
     rad = np.concatenate([rad, rng.uniform(0.1, 0.35, (batch, obstacles))], 1)
     ranges = _ray_circles(lx, ly, ang, cx, cy, rad, max_range).astype(np.float32)
     return dict(pose=pose, ranges=ranges, angle_min=amin, angle_inc=ainc, angle_max=amax, waypoints=wp)
+
+
+def drive_stream(ticks: int, seed: int = 0, step: float = 0.09, beams: int = SCAN_BEAMS, obstacles: int = 40,
+                 max_range: float = 10.0):
+    """A scripted drive for the project node's callbacks: the car follows the elliptical path
+    (4.5 m/s x 20 ms per tick = 0.09 m, src/project.cpp:233-235) with a small lateral wobble; the
+    world holds the two track walls and `obstacles` static circles beside the path. Returns
+    dict(pose [T,4] f64, ranges [T,beams] f32, geometry, waypoints [W,2])."""
+    rng = np.random.default_rng(seed)
+    wp = track_waypoints()
+    W = wp.shape[0]
+    seg = np.hypot(*(np.roll(wp, -1, 0) - wp).T)
+    s_along = np.concatenate([[0.0], np.cumsum(seg)])
+    total = s_along[-1]
+    s0 = rng.uniform(0, total)
+    s = (s0 + step * np.arange(ticks)) % total
+    k = np.searchsorted(s_along, s, side="right") - 1
+    frac = (s - s_along[k]) / seg[k]
+    nxt = wp[(k + 1) % W]
+    base = wp[k] + (nxt - wp[k]) * frac[:, None]
+    hd = np.arctan2(nxt[:, 1] - wp[k, 1], nxt[:, 0] - wp[k, 0])
+    lat = 0.2 * np.sin(np.arange(ticks) * 0.15)
+    x = base[:, 0] - np.sin(hd) * lat
+    y = base[:, 1] + np.cos(hd) * lat
+    yaw = hd + 0.05 * np.cos(np.arange(ticks) * 0.2)
+    pose = np.stack([x, y, np.sin(yaw / 2), np.cos(yaw / 2)], 1)
+    hw = np.arctan2(np.roll(wp[:, 1], -1) - wp[:, 1], np.roll(wp[:, 0], -1) - wp[:, 0])
+    nrm = np.stack([-np.sin(hw), np.cos(hw)], 1)
+    wall = np.concatenate([wp + 1.6 * nrm, wp - 1.6 * nrm])
+    oi = rng.integers(0, W, obstacles)
+    obst = wp[oi] + nrm[oi] * rng.choice([-0.9, 0.9], obstacles)[:, None]
+    cxs = np.concatenate([wall[:, 0], obst[:, 0]])
+    cys = np.concatenate([wall[:, 1], obst[:, 1]])
+    rads = np.concatenate([np.full(len(wall), 0.12), rng.uniform(0.15, 0.3, obstacles)])
+    amin, ainc, amax = scan_geometry(beams)
+    ang = yaw[:, None] + (amin + ainc * np.arange(beams, dtype=np.float64))[None, :]
+    lx, ly = x + 0.275 * np.cos(yaw), y + 0.275 * np.sin(yaw)
+    d = np.hypot(cxs[None, :] - lx[:, None], cys[None, :] - ly[:, None])
+    near = np.argsort(d, axis=1)[:, :200]
+    ranges = _ray_circles(lx, ly, ang, cxs[near], cys[near], rads[near], max_range).astype(np.float32)
+    return dict(pose=pose, ranges=ranges, angle_min=amin, angle_inc=ainc, angle_max=amax, waypoints=wp)

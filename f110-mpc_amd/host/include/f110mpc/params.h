@@ -9,6 +9,7 @@ struct Params {
   double r0 = 0.10, r1 = 5.0;             // :5-6
   int horizon = 30;                       // :12
   float dt = 0.01f;                       // :13 (MPC::dt_ is a float)
+  double dt_double = 0.01;                // :13 as Traj_Plan reads it (a double member)
   double des_vel = 4.5, des_steer = 0.0;  // :42-43
   float umax = 4.5f, umin = 3.0f;         // :46-47 (Constraints members are float)
   float follow_gap_thresh = 3.f;          // :49
@@ -19,6 +20,9 @@ struct Params {
   double steer_max = 0.4;                 // :56
   int traj_discrete = 50;                 // :57
   double lookahead = 2.5;                 // :59
+  int occ_size = 10;                      // :16 (OccGrid::size_ int)
+  float occ_discrete = 0.1f;              // :17 (float)
+  float occ_dilation = 0.15f;             // :18 (float)
   bool gap_constraints = false;           // build option: enforce the gap rows (C3 semantic)
 };
 

@@ -29,7 +29,10 @@ bool LoadParams(const std::string& path, Params* p) {
     else if (k == "r0") p->r0 = d;
     else if (k == "r1") p->r1 = d;
     else if (k == "horizon") p->horizon = static_cast<int>(d);
-    else if (k == "dt") p->dt = static_cast<float>(d);
+    else if (k == "dt") { p->dt = static_cast<float>(d); p->dt_double = d; }
+    else if (k == "occ_size") p->occ_size = static_cast<int>(d);
+    else if (k == "occ_discrete") p->occ_discrete = static_cast<float>(d);
+    else if (k == "occ_dilation") p->occ_dilation = static_cast<float>(d);
     else if (k == "des_vel") p->des_vel = d;
     else if (k == "des_steer") p->des_steer = d;
     else if (k == "umax") p->umax = static_cast<float>(d);

@@ -3,6 +3,11 @@
 //   host_demo cpu <params.yaml>                         host-only checks, JSON on stdout
 //   host_demo tick <params.yaml> <in.bin> <out.bin>     MPC::Update over T ticks (GPU)
 //   host_demo batch <params.yaml> <in.bin> <out.bin>    MPC::UpdateBatch over B candidates (GPU)
+//   host_demo project <params.yaml> <in.bin> <out.bin>  the project node's callbacks over T ticks
+//     in.bin (float64): T, R, W, angle_min, angle_inc, angle_max, waypoints[W][2], then per tick
+//     pose[4] (x, y, qz, qw) and ranges[R]; each tick = OdomCallback, ScanCallback, DriveStep.
+//     out.bin (float64) per tick: planned, plan_status, best_traj, best_global, mpc_status,
+//     drive v, drive steer, miniPath size, then the first 2N entries of MPC's u (NaN if none).
 // in.bin (float32): T, N, then per tick x0[3], u_lin[2], x_ref[N*3]; gap mode adds
 // scan geometry (3) + R ranges per tick after an R header.
 #include <cmath>
@@ -14,6 +19,7 @@
 #include <vector>
 
 #include "f110mpc/mpc.h"
+#include "f110mpc/project.h"
 
 static std::vector<float> read_all(const char* path) {
   std::ifstream f(path, std::ios::binary);
@@ -108,7 +114,56 @@ static int tick(const char* params_path, const char* in, const char* out, bool b
   return 0;
 }
 
+static int project(const char* params_path, const char* in, const char* out) {
+  Params p;
+  if (!LoadParams(params_path, &p)) return 2;
+  std::ifstream f(in, std::ios::binary);
+  f.seekg(0, std::ios::end);
+  const size_t n = static_cast<size_t>(f.tellg()) / 8;
+  f.seekg(0);
+  std::vector<double> v(n);
+  f.read(reinterpret_cast<char*>(v.data()), n * 8);
+  const int T = static_cast<int>(v[0]), R = static_cast<int>(v[1]), W = static_cast<int>(v[2]);
+  LaserScan scan;
+  scan.angle_min = static_cast<float>(v[3]);
+  scan.angle_increment = static_cast<float>(v[4]);
+  scan.angle_max = static_cast<float>(v[5]);
+  size_t o = 6;
+  std::vector<State> path;
+  for (int i = 0; i < W; i++, o += 2) path.emplace_back(v[o], v[o + 1], 0.0);
+  Project prj(p, path);
+  const int N = p.horizon;
+  std::vector<double> res;
+  for (int t = 0; t < T; t++) {
+    Pose pose;
+    pose.x = v[o]; pose.y = v[o + 1]; pose.qz = v[o + 2]; pose.qw = v[o + 3];
+    o += 4;
+    scan.ranges.assign(R, 0.f);
+    for (int r = 0; r < R; r++) scan.ranges[r] = static_cast<float>(v[o + r]);
+    o += R;
+    prj.OdomCallback(pose);   // odometry first: the first scan is only taken after a pose (:43)
+    prj.ScanCallback(scan);
+    Input drive(0, 0);
+    const bool drove = prj.DriveStep(&drive);
+    res.push_back(prj.planned_last_tick());
+    res.push_back(prj.last_plan_status());
+    res.push_back(prj.best_traj_idx());
+    res.push_back(prj.best_global_idx());
+    res.push_back(prj.mpc().last_status());
+    res.push_back(drove ? drive.v() : NAN);
+    res.push_back(drove ? drive.steer_ang() : NAN);
+    res.push_back(static_cast<double>(prj.mini_path().size()));
+    const auto& z = prj.mpc().solution();
+    const int ns = 3 * (N + 1);
+    for (int k = 0; k < 2 * N; k++) res.push_back(prj.mpc().last_status() == 1 ? z[ns + k] : NAN);
+  }
+  std::ofstream fo(out, std::ios::binary);
+  fo.write(reinterpret_cast<const char*>(res.data()), res.size() * 8);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 5 && !std::strcmp(argv[1], "project")) return project(argv[2], argv[3], argv[4]);
   if (argc >= 3 && !std::strcmp(argv[1], "cpu")) return cpu(argv[2]);
   if (argc >= 5 && !std::strcmp(argv[1], "tick")) return tick(argv[2], argv[3], argv[4], false);
   if (argc >= 5 && !std::strcmp(argv[1], "batch")) return tick(argv[2], argv[3], argv[4], true);

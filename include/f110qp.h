@@ -190,6 +190,14 @@ int f110qp_plan_batch_dev(const f110qp_plan_config* cfg, int batch, const double
                           unsigned char* valid, int* best_global, int* best_traj, float* x_ref,
                           float* x0, int* status, void* stream);
 
+/* Same on host pointers (synchronous; device buffers are cached per host thread). table and
+ * waypoints are host arrays too. Used by the ROS-free host mirror for one scenario per tick. */
+int f110qp_plan_batch(const f110qp_plan_config* cfg, int batch, const double* pose,
+                      const float* ranges, int num_ranges, float angle_min, float angle_increment,
+                      float angle_max, const double* table, const double* waypoints,
+                      int num_waypoints, unsigned char* grid, unsigned char* valid,
+                      int* best_global, int* best_traj, float* x_ref, float* x0, int* status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -100,3 +100,94 @@ def test_mpc_update_batch_candidates(demo, oracle, tmp_path):
                                               np.repeat(np.float32([[4.5, 0.1]]), 31, 0), xr)
     np.testing.assert_array_equal(st, st_ref)
     assert np.abs(u - u_ref).max() <= 1e-4 * 4.5
+
+
+def _emulate_project(oracle, d, N=30):
+    """project::OdomCallback / ScanCallback / DriveLoop (src/project.cpp:41-236) in Python over
+    the oracle's planner and exact solver (the deviation of the host mirror is kept: the grid is
+    built at planning time from the latest scan at the planning pose)."""
+    pp = oracle.plan_params()
+    table = oracle.traj_table(pp)
+    prm = oracle.params(N)
+    st = dict(first_pose=False, first_scan=False, have_scan=False, get_mini=False, mini=[], inputs=[], idx=0,
+              scan=None, sol=None)
+    rows = []
+    for t in range(d["pose"].shape[0]):
+        pose = d["pose"][t]
+        st["first_pose"] = True
+        planned, pstat, bt, bg, mstat = 0, -1 if t == 0 else rows[-1][1], None, None, 0
+        bt = rows[-1][2] if rows else -1
+        bg = rows[-1][3] if rows else -1
+        mstat = rows[-1][4] if rows else 0
+        if not st["get_mini"]:
+            if st["have_scan"]:
+                g, off = oracle.fill_occ_grid(pp, pose, st["scan"], d["angle_min"], d["angle_inc"], d["angle_max"])
+                r = oracle.plan(pp, pose, g, off, table, d["waypoints"])
+                planned, pstat, bt, bg = 1, r["status"], r["best_traj"], r["best_global"]
+                if r["status"] == 0:
+                    st["mini"] = [tuple(p) for p in r["x_ref"]]
+                    st["get_mini"] = True
+        elif st["first_scan"]:
+            inp = st["inputs"][st["idx"]] if st["idx"] < len(st["inputs"]) else (0.5, 0.0)
+            ul = np.float32([4.5, inp[1]])
+            cur = oracle.lib().f110o_car_orientation(np.ascontiguousarray(pose).ctypes.data_as(
+                __import__("ctypes").POINTER(__import__("ctypes").c_double)))
+            end = np.float32(st["mini"][-1][:2])
+            car = np.float32(pose[:2])
+            if np.float32(np.sqrt(np.float64(car[0] - end[0]) ** 2 + np.float64(car[1] - end[1]) ** 2)) < 1.98:
+                st["get_mini"] = False
+                st["mini"] = []
+            mstat = 0
+            if len(st["mini"]) >= N:
+                x0 = np.float32([pose[0], pose[1], cur])
+                xr = np.float32(st["mini"][:N])
+                u, x, s_ = oracle.solve_batch(prm, x0[None], ul[None], xr[None])
+                mstat = int(s_[0])
+                if mstat == 1:
+                    st["sol"] = u[0]
+            if st["sol"] is not None:
+                st["inputs"] = [tuple(v) for v in np.float32(st["sol"]).astype(np.float64)]
+            st["idx"] = 0
+        # ScanCallback (:41-56)
+        if st["first_pose"]:
+            st["first_scan"] = True
+            st["have_scan"] = True
+            st["scan"] = d["ranges"][t]
+        drive = (np.nan, np.nan)
+        if st["first_pose"] and st["first_scan"]:
+            drive = st["inputs"][st["idx"]] if st["idx"] < len(st["inputs"]) else (0.5, 0.0)
+            st["idx"] += 1
+        rows.append((planned, pstat, bt, bg, mstat, drive[0], drive[1], len(st["mini"])))
+    return rows
+
+
+@pytest.mark.gpu
+def test_project_callbacks_drive_the_tick(demo, oracle, tmp_path):
+    """The ROS-free project mirror (host/src/project.cpp) over a scripted drive: planning on the
+    device (f110qp_plan_batch), MPC::Update on the device, the DriveLoop's inputs. Plan
+    decisions equal the oracle's exactly, inputs and MPC solutions within the QP tolerance."""
+    T = 90
+    d = workload.drive_stream(T, seed=4)
+    R = d["ranges"].shape[1]
+    W = d["waypoints"].shape[0]
+    header = np.array([T, R, W, d["angle_min"], d["angle_inc"], d["angle_max"]], np.float64)
+    body = [d["waypoints"][:, :2].ravel()]
+    for t in range(T):
+        body += [d["pose"][t], d["ranges"][t].astype(np.float64)]
+    inp = tmp_path / "prj.bin"
+    np.concatenate([header] + body).astype(np.float64).tofile(inp)
+    outp = tmp_path / "prj_out.bin"
+    subprocess.check_call([demo, "project", PARAMS, str(inp), str(outp)])
+    N = 30
+    res = np.fromfile(outp, np.float64).reshape(T, 8 + 2 * N)
+    ref = _emulate_project(oracle, d, N)
+    replans = 0
+    for t in range(T):
+        got, exp = res[t], ref[t]
+        assert tuple(int(v) for v in got[:5]) == tuple(int(v) for v in exp[:5]), (t, got[:8], exp)
+        assert int(got[7]) == exp[7], t
+        replans += int(got[0])
+        if not np.isnan(exp[5]):
+            assert abs(got[5] - exp[5]) <= 1e-4 * max(1.0, abs(exp[5])) and abs(got[6] - exp[6]) <= 1e-4, (t, got[5:7], exp[5:7])
+    # plan, two MPC ticks, then the 1.98 m trigger clears the path: ~2 solves per 4 ticks
+    assert replans >= 2 and (res[:, 4] == 1).sum() >= T // 3
