@@ -350,6 +350,8 @@ struct Smem {
   float cmult[3 * VN];             // multiplier per constraint id
   int ids[VN];                     // PDAS: constraint id of each active slot
   float pmu[VN];                   // PDAS: multiplier of each variable's active bound
+  alignas(16) float prow[NUM];     // box PDAS: pivot row of T broadcast (pivot_T)
+  alignas(16) float yb[NUM];       // box PDAS: right-hand side broadcast (matvec_T)
   double d64[VN];
   double sx64[NST], sy64[NST];
   Lin M;                           // linearisation of this QP (uniform)
@@ -518,6 +520,7 @@ __device__ __forceinline__ float vcol(Smem<NUM, GAP>& sm, int j, int sid_j, int 
 // with f = 1 - 1/a_pp. After all pivots the rows hold -H^-1. P is a template constant so every
 // register index is static (no scratch).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int NUM, int R, int P>
 __device__ __forceinline__ void sweep_step(float (&hrow)[R][NUM], int lane) {
@@ -556,6 +559,89 @@ template <int NUM, int R>
 struct Sweep<NUM, R, NUM> {
   static __device__ __forceinline__ void run(float (&)[R][NUM], int) {}
 };
+
+// ---- box rows: the partially swept Hessian T (rows in registers) --------------------------
+// T = SWP_F(H), the sweep of H on the free set F: T_FF = -(H_FF)^-1, T_FA = H_FF^-1 H_FA and
+// T_AA = H_AA - H_AF H_FF^-1 H_FA (the full sweep above leaves F = all, T = -H^-1). Moving one
+// variable k between F and the active set A is one sweep (sg = +1, A -> F) or reverse sweep
+// (sg = -1, F -> A) pivot on k: a rank-1 update of the register rows, no factorization, and a
+// box-constrained solve of a guess A is one product with T (matvec_T).
+// The pivot row is broadcast through LDS with its entry k replaced by T_kk - sg, so the common
+// FMA leaves sg * T_ik / T_kk in column k of every other row. The pivot lane's own diagonal
+// entry then ends 2 sg away from -1/T_kk: the exact diagonal is carried in dg, and ed (a small
+// integer, exact in fp32) records the offset of the register copy, which matvec_T removes.
+template <int NUM, bool GAP, int R>
+__device__ __forceinline__ void pivot_T(Smem<NUM, GAP>& sm, float (&h)[R][NUM], float (&dg)[R],
+                                        float (&ed)[R], int lane, const int (&vv)[R], int k,
+                                        float sg) {
+  const int kl = k & 63, kr = k >> 6;
+  if (lane == kl) {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (r == kr) {
+#pragma unroll
+        for (int j = 0; j < NUM; j += 4)
+          *reinterpret_cast<f32x4*>(&sm.prow[j]) = f32x4{h[r][j], h[r][j + 1], h[r][j + 2], h[r][j + 3]};
+        sm.prow[k] = dg[r] - sg;
+      }
+    }
+  }
+  wsync();
+  float rk[NUM];
+#pragma unroll
+  for (int j = 0; j < NUM; j += 4) {
+    const f32x4 v4 = *reinterpret_cast<const f32x4*>(&sm.prow[j]);
+    rk[j] = v4.x; rk[j + 1] = v4.y; rk[j + 2] = v4.z; rk[j + 3] = v4.w;
+  }
+  float tk[R];  // T_ki = T_ik (symmetric) of this lane's rows
+#pragma unroll
+  for (int r = 0; r < R; r++) tk[r] = (vv[r] < NUM) ? sm.prow[vv[r]] : 0.f;
+  const float inv = __builtin_amdgcn_rcpf(readlane_f(pick<R>(dg, kr), kl));
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const bool piv = (r == kr) && (lane == kl);
+    const float f = piv ? fmaf(-sg, inv, 1.f) : tk[r] * inv;
+    const f32x2 nf = {-f, -f};
+#pragma unroll
+    for (int j = 0; j < NUM; j += 2) {
+      f32x2 x = {h[r][j], h[r][j + 1]};
+      x = __builtin_elementwise_fma(nf, f32x2{rk[j], rk[j + 1]}, x);
+      h[r][j] = x.x;
+      h[r][j + 1] = x.y;
+    }
+    dg[r] = piv ? -inv : fmaf(-f, tk[r], dg[r]);
+    ed[r] += piv ? 2.f * sg : 0.f;
+  }
+  wsync();  // prow is rewritten by the next pivot
+}
+
+// x = T y (y one entry per variable, zero outside the valid rows)
+template <int NUM, bool GAP, int R>
+__device__ __forceinline__ void matvec_T(Smem<NUM, GAP>& sm, const float (&h)[R][NUM],
+                                         const float (&ed)[R], const int (&vv)[R],
+                                         const float (&y)[R], float (&x)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; r++)
+    if (vv[r] < NUM) sm.yb[vv[r]] = y[r];
+  wsync();
+  float yb[NUM];
+#pragma unroll
+  for (int j = 0; j < NUM; j += 4) {
+    const f32x4 v4 = *reinterpret_cast<const f32x4*>(&sm.yb[j]);
+    yb[j] = v4.x; yb[j + 1] = v4.y; yb[j + 2] = v4.z; yb[j + 3] = v4.w;
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    f32x2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NUM; j += 4) {
+      a0 = __builtin_elementwise_fma(f32x2{h[r][j], h[r][j + 1]}, f32x2{yb[j], yb[j + 1]}, a0);
+      a1 = __builtin_elementwise_fma(f32x2{h[r][j + 2], h[r][j + 3]}, f32x2{yb[j + 2], yb[j + 3]}, a1);
+    }
+    x[r] = fmaf(-ed[r], y[r], (a0.x + a0.y) + (a1.x + a1.y));
+  }
+  wsync();  // yb is rewritten by the next product
+}
 
 // Build the slots of the bound guess act (0 free, 1 lower, 2 upper) in variable order and
 // factor S_A. Returns the slot count.
@@ -711,6 +797,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   STAMP(t_grad);
   STAMP(t_hess);
   STAMP(t_inv);
+  float hrow[R][NUM];  // condensed Hessian rows, swept in place to T = -H^-1 (box path keeps it)
   if (whit) {
     // ---- 2b/3 (warm hit): W from the slot cache, no Hessian, no sweep ------------------
     const float* Wc = ws.W + (size_t)b * NU * NU;
@@ -725,6 +812,12 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       }
     }
     wsync();
+    if constexpr (!GAP) {
+#pragma unroll
+      for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int j = 0; j < NUM; j++) hrow[r][j] = (vv[r] < NUM) ? -sm.W[j][vv[r]] : 0.f;
+    }
   } else {
   // ---- 2b. condensed Hessian rows (closed form, fp32) -------------------------------------
   // Row v = (k, a), column w = (l, b). For l <= k the stages that see both inputs are
@@ -732,7 +825,6 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   //   H[v][w] = C0_b + C1_b * (k - l)
   // with four per-row constants (sums of 1, t, t^2 over the T stages). The entries with
   // l > k are the transpose: every lane publishes its lower rows and reads column v back.
-  float hrow[R][NUM];
   {
     const Lin M = sm.M;
     const float fa02 = (float)M.a02, fa12 = (float)M.a12, fb00 = (float)M.b00;
@@ -822,19 +914,13 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 
   STAMP_SET(t_inv);
   // ---- 4. active set -----------------------------------------------------------------------
-  // x = -W g  (g in sm.vec)
-  float xv[R];
-  matvec_W<NUM, GAP, R>(sm, lane, xv);
-#pragma unroll
-  for (int r = 0; r < R; r++) xv[r] = valid[r] ? -xv[r] : 0.f;
-  wsync();
-
+  float xv[R];           // GI iterate (fp32)
   int actf[R];           // bit t set when constraint 3*v+t is active
   int slot_id[R];        // constraint id of active slot (64r + lane), -1 if none
   float mult[R];         // its multiplier
   float rdiag[R];        // 1 / L[slot][slot]
 #pragma unroll
-  for (int r = 0; r < R; r++) { actf[r] = 0; slot_id[r] = -1; mult[r] = 0.f; rdiag[r] = 0.f; }
+  for (int r = 0; r < R; r++) { xv[r] = 0.f; actf[r] = 0; slot_id[r] = -1; mult[r] = 0.f; rdiag[r] = 0.f; }
   int q = 0;
   int it = 0;
   const int max_iter = P.max_iter;
@@ -845,149 +931,172 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #pragma unroll
   for (int r = 0; r < R; r++) u64[r] = 0.0;
   bool final_ok = false;
+  bool gi_start = true;  // GI starts from the unconstrained point (x = -W g)
   int forced_p = -1;     // violated row found by the fp64 re-check
   float forced_sp = 0.f;
 
-  // ---- 4a. box rows only: primal-dual active set warm start (Hintermueller-Ito-Kunisch) ----
-  // Each pass solves the equality QP of the current guess by one Schur solve with S_A =
-  // W[A][A] and re-guesses A from the multipliers and the bounds; on these QPs it reaches
-  // the optimal set in <= 5 passes (one-at-a-time GI needs one pass per active bound). Its
-  // fixed point is a valid GI state (independent normals, positive multipliers), so the GI
-  // loop below only confirms it, and resumes from it if the fp64 re-check finds a violated
-  // row. No convergence within kPdasMaxIter passes -> plain GI from the unconstrained point.
-  if (!GAP && status == F110QP_SOLVED_ID) {
-    STAMP(t_pdas);
-    constexpr int kPdasMaxIter = 10;
-    float uunc[R], u[R], mu[R];
-    int act[R];          // 0 free, 1 at the lower bound, 2 at the upper bound
-    int sid[R];          // slot lanes: constraint id of the slot
-    float rdp[R];        // slot lanes: 1 / L[j][j]
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      uunc[r] = xv[r];
-      u[r] = xv[r];
-      mu[r] = 0.f;
-      sm.vec[vv[r]] = uunc[r];
-      act[r] = 0;
-      sid[r] = -1;
-      rdp[r] = 0.f;
-      if (warm && wvalid && valid[r]) {  // previous tick's active bounds seed the first guess
-        const unsigned long long lo_m = ws.act[2 * (R * b + r)], hi_m = ws.act[2 * (R * b + r) + 1];
-        act[r] = ((lo_m >> lane) & 1ull) ? 1 : (((hi_m >> lane) & 1ull) ? 2 : 0);
-      }
-    }
-    int qn = 0;            // slots of the current guess
-    bool converged = false;
-    bool seeded = false;   // warm guess: build its slots before the first solve
-#pragma unroll
-    for (int r = 0; r < R; r++) seeded = seeded || (__ballot(act[r] != 0) != 0);
-    wsync();
-    for (int pit = 0; pit < kPdasMaxIter; pit++) {
-      if (seeded) {
-        seeded = false;
-        qn = build_box_slots<NUM, GAP, R>(sm, lane, act, sid, rdp);
-      }
-      // solve the equality QP of the current slots: mu = S^-1 (b - N'u_unc), u = u_unc + W N mu
-      float rhs[R];
+  // ---- 4a. box rows only: primal-dual active set (Hintermueller-Ito-Kunisch) on T ----------
+  // Each pass solves the equality QP of the current guess A with one product x = T y
+  // (y = g on F, -bound on A): u_F = x_F, and the bound multipliers are lambda_A = g_A - x_A
+  // (lambda = Hu + g). The next guess follows from the multipliers and the bounds; each
+  // variable that enters or leaves A is one pivot of T. On these QPs the optimal set is
+  // reached in <= 5 passes. The fixed point is then refined in fp64 (residual from the fp64
+  // rollout and costate, correction through T on F) and re-checked exactly; a violated row
+  // hands the set over to the GI loop below as a valid GI state (independent normals,
+  // positive multipliers). No convergence within kPdasMaxIter passes -> plain GI from the
+  // unconstrained point.
+  if constexpr (!GAP) {
+    if (status == F110QP_SOLVED_ID) {
+      STAMP(t_pdas);
+      constexpr int kPdasMaxIter = 10;
+      float dg[R], ed[R], gr[R], u[R], lam[R];
+      int act[R];  // 0 free, 1 at the lower bound, 2 at the upper bound
 #pragma unroll
       for (int r = 0; r < R; r++) {
-        rhs[r] = 0.f;
-        if (64 * r + lane < qn) {
-          const int sv = sid[r] / 3;
-          const float sg = box_sign(sid[r]);
-          const float bj = (sg > 0.f) ? ((sv & 1) ? umin1 : umin0) : -((sv & 1) ? umax1 : umax0);
-          rhs[r] = bj - sg * sm.vec[sv];
+        dg[r] = (vv[r] < NUM) ? -sm.W[vv[r]][vv[r]] : 0.f;
+        ed[r] = 0.f;
+        gr[r] = valid[r] ? sm.vec[vv[r]] : 0.f;
+        u[r] = 0.f;
+        lam[r] = 0.f;
+        act[r] = 0;
+        if (warm && wvalid && valid[r]) {  // previous tick's active bounds seed the first guess
+          const unsigned long long lo_m = ws.act[2 * (R * b + r)], hi_m = ws.act[2 * (R * b + r) + 1];
+          act[r] = ((lo_m >> lane) & 1ull) ? 1 : (((hi_m >> lane) & 1ull) ? 2 : 0);
         }
       }
-      float lvp[R];
-      tri_forward<NUM, GAP, R>(sm, lane, qn, rdp, rhs, lvp);
-      tri_backward<NUM, GAP, R>(sm, lane, qn, rdp, lvp, mu);
 #pragma unroll
-      for (int r = 0; r < R; r++) u[r] = uunc[r];
-      for (int j = 0; j < qn; j++) {
-        const int sj = rl_i<R>(sid, j);
-        const float mj = rl_f<R>(mu, j) * box_sign(sj);
-        const float* wr = sm.W[sj / 3];
-#pragma unroll
-        for (int r = 0; r < R; r++) u[r] = fmaf(mj, wr[cl[r]], u[r]);
+      for (int r0 = 0; r0 < R; r0++) {
+        unsigned long long m = __ballot(act[r0] != 0);
+        while (m) {
+          const int bit = __builtin_ctzll(m);
+          m &= m - 1;
+          pivot_T<NUM, GAP, R>(sm, hrow, dg, ed, lane, vv, 64 * r0 + bit, -1.f);
+        }
       }
+      bool converged = false;
+      for (int pit = 0; pit < kPdasMaxIter; pit++) {
+        float y[R], x[R];
 #pragma unroll
-      for (int r = 0; r < R; r++)
-        if (64 * r + lane < qn) sm.pmu[sid[r] / 3] = mu[r];
-      wsync();
-      int nact[R];
-      unsigned long long changed[R];
-      bool any_changed = false, leaves = false;
+        for (int r = 0; r < R; r++)
+          y[r] = !valid[r] ? 0.f : (act[r] == 1 ? -lb[r] : (act[r] == 2 ? -ub[r] : gr[r]));
+        matvec_T<NUM, GAP, R>(sm, hrow, ed, vv, y, x);
+        int nact[R];
+        bool any_changed = false;
 #pragma unroll
-      for (int r = 0; r < R; r++) {
-        const float myu = act[r] ? sm.pmu[vv[r]] : 0.f;
-        const bool nlo = valid[r] && ((act[r] == 1 ? myu : 0.f) + (lb[r] - u[r]) > 0.f);
-        const bool nhi = valid[r] && !nlo && ((act[r] == 2 ? myu : 0.f) + (u[r] - ub[r]) > 0.f);
-        nact[r] = nlo ? 1 : (nhi ? 2 : 0);
-        changed[r] = __ballot(nact[r] != act[r]);
-        any_changed = any_changed || changed[r] != 0;
-        leaves = leaves || (__ballot(act[r] != 0 && nact[r] != act[r]) != 0);
-      }
-      if (!any_changed) { converged = true; it = pit + 1; break; }
-      if (qn == 0 || leaves) {
-        // first guess, or a slot leaves / flips side: build slots and chol(S_A) from scratch
-        qn = build_box_slots<NUM, GAP, R>(sm, lane, nact, sid, rdp);
-      } else {
-        // only additions: append each new bound as a slot with one forward solve
-        // (incremental Cholesky row l = L^-1 S[q][:q], L[q][q] = sqrt(S[q][q] - l'l))
+        for (int r = 0; r < R; r++) {
+          u[r] = !valid[r] ? 0.f : (act[r] == 1 ? lb[r] : (act[r] == 2 ? ub[r] : x[r]));
+          lam[r] = (valid[r] && act[r]) ? gr[r] - x[r] : 0.f;
+          const float myu = act[r] == 1 ? lam[r] : (act[r] == 2 ? -lam[r] : 0.f);
+          const bool nlo = valid[r] && ((act[r] == 1 ? myu : 0.f) + (lb[r] - u[r]) > 0.f);
+          const bool nhi = valid[r] && !nlo && ((act[r] == 2 ? myu : 0.f) + (u[r] - ub[r]) > 0.f);
+          nact[r] = nlo ? 1 : (nhi ? 2 : 0);
+          any_changed = any_changed || (__ballot(nact[r] != act[r]) != 0);
+        }
+        if (!any_changed) { converged = true; it = pit + 1; break; }
 #pragma unroll
         for (int r0 = 0; r0 < R; r0++) {
-          unsigned long long addm = changed[r0];
-          while (addm) {
-            const int bit = __builtin_ctzll(addm);
-            addm &= addm - 1;
-            const int v = 64 * r0 + bit;
-            const int na = readlane_i(nact[r0], bit);
-            const int nid = 3 * v + (na == 2 ? 1 : 0);
-            const float sg = (na == 1) ? 1.f : -1.f;
-            float sv[R], lrow[R];
-            float ll = 0.f;
-#pragma unroll
-            for (int r = 0; r < R; r++)
-              sv[r] = (64 * r + lane < qn) ? sg * box_sign(sid[r]) * sm.W[v][sid[r] / 3] : 0.f;
-            tri_forward<NUM, GAP, R>(sm, lane, qn, rdp, sv, lrow);
-#pragma unroll
-            for (int r = 0; r < R; r++) ll += (64 * r + lane < qn) ? lrow[r] * lrow[r] : 0.f;
-            ll = wave_sum(ll);
-            const float dnew = sqrtf(sm.W[v][v] - ll);
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-              const int s = 64 * r + lane;
-              if (s < qn) sm.L[qn][s] = lrow[r];
-              if (s == qn) {
-                sm.L[qn][qn] = dnew;
-                sid[r] = nid;
-                rdp[r] = 1.f / dnew;
-              }
-            }
-            qn++;
-            wsync();
+          unsigned long long enter = __ballot(act[r0] == 0 && nact[r0] != 0);
+          unsigned long long leave = __ballot(act[r0] != 0 && nact[r0] == 0);
+          while (enter) {
+            const int bit = __builtin_ctzll(enter);
+            enter &= enter - 1;
+            pivot_T<NUM, GAP, R>(sm, hrow, dg, ed, lane, vv, 64 * r0 + bit, -1.f);
+          }
+          while (leave) {
+            const int bit = __builtin_ctzll(leave);
+            leave &= leave - 1;
+            pivot_T<NUM, GAP, R>(sm, hrow, dg, ed, lane, vv, 64 * r0 + bit, 1.f);
           }
         }
-      }
 #pragma unroll
-      for (int r = 0; r < R; r++) act[r] = nact[r];
-    }
-    if (converged) {
-      // hand the active set to the GI state: slots, multipliers, chol(S_A)
-      q = qn;
-#pragma unroll
-      for (int r = 0; r < R; r++) {
-        const bool sl = 64 * r + lane < qn;
-        slot_id[r] = sl ? sid[r] : -1;
-        mult[r] = sl ? fmaxf(mu[r], 0.f) : 0.f;
-        rdiag[r] = sl ? rdp[r] : 0.f;
-        actf[r] = act[r];  // bit0 lower, bit1 upper
-        xv[r] = valid[r] ? u[r] : 0.f;
+        for (int r = 0; r < R; r++) act[r] = nact[r];
       }
-      wsync();
+      STAMP_ACC(acc_pdas, t_pdas);
+      if (converged) {
+        STAMP(t_ref0);
+        // fp64 refinement: r1 = Hu + g on F from the fp64 rollout and costate, du_F = T_FF r1_F
+        const Lin M = sm.M;
+        double rxd[R], ryd[R], rthd[R], zero[R], px[R], py[R], th[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          rxd[r] = sm.rx[vv[r]]; ryd[r] = sm.ry[vv[r]]; rthd[r] = sm.rth[vv[r]];
+          zero[r] = 0.0;
+          u64[r] = valid[r] ? (double)u[r] : 0.0;  // active entries are the bounds exactly
+        }
+        for (int rs = 0; rs < 2; rs++) {
+          double r1[R];
+          rollout_f64<R>(M, lane, u64, px, py, th);
+          grad_f64<R>(M, P, lane, N, u64, px, py, th, rxd, ryd, rthd, zero, zero, r1);
+          float y[R], dx[R];
+#pragma unroll
+          for (int r = 0; r < R; r++) y[r] = (valid[r] && !act[r]) ? (float)r1[r] : 0.f;
+          matvec_T<NUM, GAP, R>(sm, hrow, ed, vv, y, dx);
+          float adx = 0.f;
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            const bool fr = valid[r] && !act[r];
+            if (fr) u64[r] += (double)dx[r];
+            adx = fmaxf(adx, fr ? fabsf(dx[r]) : 0.f);
+          }
+          int dummy = 0;
+          adx = -adx;
+          wave_argmin(adx, dummy);  // -max |dx|
+          if (-adx <= 1e-5f) break;
+        }
+        // exact feasibility re-check of the free variables at the refined point
+        float best64 = 0.f, sp64 = 0.f;
+        int bid64 = 0x7fffffff;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          if (!valid[r] || act[r]) continue;
+          const int v = vv[r];
+          const double s0 = u64[r] - (double)lb[r], s1 = (double)ub[r] - u64[r];
+          const float v0 = (float)(s0 / (1.0 + fabs((double)lb[r])));
+          const float v1 = (float)(s1 / (1.0 + fabs((double)ub[r])));
+          if (v0 < -1e-9f && v0 < best64) { best64 = v0; bid64 = 3 * v; sp64 = (float)s0; }
+          if (v1 < -1e-9f && v1 < best64) { best64 = v1; bid64 = 3 * v + 1; sp64 = (float)s1; }
+        }
+        wave_argmin(best64, bid64);
+#pragma unroll
+        for (int r = 0; r < R; r++) actf[r] = act[r];  // bit0 lower, bit1 upper
+        STAMP_ACC(acc_refine, t_ref0);
+        if (bid64 == 0x7fffffff) {
+          final_ok = true;
+        } else {
+          // hand the set to the GI state: slots, chol(S_A), multipliers, the violated row
+          int sid[R];
+          float rdp[R];
+          q = build_box_slots<NUM, GAP, R>(sm, lane, act, sid, rdp);
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            if (valid[r]) sm.pmu[vv[r]] = act[r] == 1 ? lam[r] : -lam[r];
+            xv[r] = valid[r] ? (float)u64[r] : 0.f;
+          }
+          wsync();
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            const bool sl = 64 * r + lane < q;
+            slot_id[r] = sl ? sid[r] : -1;
+            mult[r] = sl ? fmaxf(sm.pmu[sid[r] / 3], 0.f) : 0.f;
+            rdiag[r] = sl ? rdp[r] : 0.f;
+          }
+          reentries = 1;
+          forced_p = bid64;
+          forced_sp = readlane_f(sp64, (bid64 / 3) & 63);
+          gi_start = false;
+          wsync();
+        }
+      }
     }
-    STAMP_ACC(acc_pdas, t_pdas);
+  }
+  if (gi_start && !final_ok) {
+    // x = -W g  (g in sm.vec)
+    matvec_W<NUM, GAP, R>(sm, lane, xv);
+#pragma unroll
+    for (int r = 0; r < R; r++) xv[r] = valid[r] ? -xv[r] : 0.f;
+    wsync();
+#pragma unroll
+    for (int r = 0; r < R; r++) actf[r] = 0;
   }
 
   // ---- 4b. dual active set (Goldfarb-Idnani, range space) ---------------------------------
