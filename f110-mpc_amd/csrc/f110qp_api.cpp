@@ -143,6 +143,12 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     const int v = std::atoi(em);
     if (v >= 0 && v <= 4) c->lane_mode = v;
   }
+  // test hook: F110QP_PDAS_MAX caps the wave kernel's box PDAS passes (0 = GI from scratch)
+  k.pdas_max = 10;
+  if (const char* ep = std::getenv("F110QP_PDAS_MAX")) {
+    const int v = std::atoi(ep);
+    if (v >= 0 && v <= 64) k.pdas_max = v;
+  }
   const int nu = 2 * cfg->horizon;
   k.max_iter = cfg->max_iter > 0 ? cfg->max_iter : 8 * (nu + (cfg->gap_mode ? nu : 0)) + 16;
   k.xr_stride = cfg->x_ref_points > 0 ? cfg->x_ref_points : cfg->horizon;

@@ -22,6 +22,7 @@ struct KParams {
   float umax[2];  // input upper bounds
   int max_iter;   // active-set iteration cap
   int xr_stride;  // points per QP in x_ref (>= N; the reference passes its whole miniPath)
+  int pdas_max;   // PDAS passes of the wave kernel's box path before its GI loop takes over
 };
 
 // Warm-start state of a context (all null = cold solve). Per QP slot b of the batch:

@@ -702,36 +702,29 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #endif
   // ---- 1. inputs + Model::Linearize ----------------------------------------------------
   const float fX0 = x0g[3 * b + 0], fY0 = x0g[3 * b + 1], fTH0 = x0g[3 * b + 2];
+  const float ul0 = ulg[2 * b + 0], ul1 = ulg[2 * b + 1];
   const double X0 = (double)fX0, Y0 = (double)fY0;
-  // non-finite data -> F110QP_NUMERICAL with NaN outputs (e.g. the NaN x_ref the planning stage
-  // emits for a scenario without a valid candidate, where the reference skips MPC::Update)
-  bool bad = !(isfinite(fX0) && isfinite(fY0) && isfinite(fTH0) && isfinite(ulg[2 * b]) &&
-               isfinite(ulg[2 * b + 1]));
-  if (lane == 0) {
-    const float* x00 = xrg + (size_t)b * P.xr_stride * 3;
-    bad = bad || !(isfinite(x00[0]) && isfinite(x00[1]) && isfinite(x00[2]));
-  }
-  {
-    const Lin M = linearize((double)fTH0, (double)ulg[2 * b + 0], (double)ulg[2 * b + 1], P.dt);
-    if (lane == 0) sm.M = M;
-    // reference point of the variable's state stage i = k+1 (terminal reuses x_ref[N-1],
-    // mpc.cpp:228), recentred in fp64.
+  // The reference point of each variable's state stage (i = k+1; the terminal stage reuses
+  // x_ref[N-1], mpc.cpp:228) is loaded here and consumed after the inverse: H depends only on
+  // the linearisation point, so the load latency hides behind the Hessian and the sweep.
+  float xrv[R][3], x00[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      double rx = 0.0, ry = 0.0;
-      float rth = 0.f;
-      if (valid[r]) {
-        const int ri = (kk[r] + 1 < N) ? kk[r] + 1 : N - 1;
-        const float* xr = xrg + ((size_t)b * P.xr_stride + ri) * 3;
-        rx = (double)xr[0] - X0;
-        ry = (double)xr[1] - Y0;
-        rth = xr[2];
-        bad = bad || !(isfinite(xr[0]) && isfinite(xr[1]) && isfinite(xr[2]));
-      }
-      sm.rx[vv[r]] = rx; sm.ry[vv[r]] = ry; sm.rth[vv[r]] = rth;
+  for (int r = 0; r < R; r++) {
+    xrv[r][0] = 0.f; xrv[r][1] = 0.f; xrv[r][2] = 0.f;
+    if (valid[r]) {
+      const int ri = (kk[r] + 1 < N) ? kk[r] + 1 : N - 1;
+      const float* xr = xrg + ((size_t)b * P.xr_stride + ri) * 3;
+      xrv[r][0] = xr[0]; xrv[r][1] = xr[1]; xrv[r][2] = xr[2];
     }
   }
-  const bool numerical = __ballot(bad) != 0ull;
+  if (lane == 0) {
+    const float* xq = xrg + (size_t)b * P.xr_stride * 3;
+    x00[0] = xq[0]; x00[1] = xq[1]; x00[2] = xq[2];
+  }
+  {
+    const Lin M = linearize((double)fTH0, (double)ul0, (double)ul1, P.dt);
+    if (lane == 0) sm.M = M;
+  }
   const float umin0 = P.umin[0], umin1 = P.umin[1], umax0 = P.umax[0], umax1 = P.umax[1];
   float lb[R], ub[R];
 #pragma unroll
@@ -762,21 +755,33 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   if (warm) {
     const unsigned* key = ws.key + 4 * b;
     wvalid = key[3] == 1u;
-    whit = wvalid && key[0] == __float_as_uint(fTH0) && key[1] == __float_as_uint(ulg[2 * b + 0]) &&
-           key[2] == __float_as_uint(ulg[2 * b + 1]);
+    whit = wvalid && key[0] == __float_as_uint(fTH0) && key[1] == __float_as_uint(ul0) &&
+           key[2] == __float_as_uint(ul1);
   }
   STAMP(t_lin);
-  // ---- 2a. gradient at u = 0 (fp64 adjoint) and the free response ------------------------
+  // ---- 2a. (run after the inverse) non-finite check, recentred references, gradient at u = 0
+  // by the fp64 adjoint, and the free response of the gap rows
+  bool numerical = false;
   float cgap[R], gnorm = 1.f;
-  {
+  auto inputs_and_gradient = [&]() {
+    // non-finite data -> F110QP_NUMERICAL with NaN outputs (e.g. the NaN x_ref the planning
+    // stage emits for a scenario without a valid candidate, where the reference skips
+    // MPC::Update)
+    bool bad = !(isfinite(fX0) && isfinite(fY0) && isfinite(fTH0) && isfinite(ul0) && isfinite(ul1));
+    if (lane == 0) bad = bad || !(isfinite(x00[0]) && isfinite(x00[1]) && isfinite(x00[2]));
     const Lin M = sm.M;
     double zero[R], px0[R], py0[R], th0s[R], rxd[R], ryd[R], rthd[R], g64[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
+      if (valid[r]) bad = bad || !(isfinite(xrv[r][0]) && isfinite(xrv[r][1]) && isfinite(xrv[r][2]));
       zero[r] = 0.0;
-      rxd[r] = sm.rx[vv[r]]; ryd[r] = sm.ry[vv[r]]; rthd[r] = sm.rth[vv[r]];
+      rxd[r] = valid[r] ? (double)xrv[r][0] - X0 : 0.0;  // recentred in fp64
+      ryd[r] = valid[r] ? (double)xrv[r][1] - Y0 : 0.0;
+      rthd[r] = (double)xrv[r][2];
+      sm.rx[vv[r]] = rxd[r]; sm.ry[vv[r]] = ryd[r]; sm.rth[vv[r]] = xrv[r][2];
       cgap[r] = 0.f;
     }
+    numerical = __ballot(bad) != 0ull;
     rollout_f64<R>(M, lane, zero, px0, py0, th0s);
     // cross-lane helpers run with all 64 lanes active (variables >= 2N contribute zeros)
     grad_f64<R>(M, P, lane, N, zero, px0, py0, th0s, rxd, ryd, rthd, zero, zero, g64);
@@ -792,9 +797,9 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       for (int r = 0; r < R; r++) cgap[r] = (float)(gah * px0[r] + gbh * py0[r] - gbe);  // slack = a X + b Y + cgap
       gnorm = (float)sqrt(gah * gah + gbh * gbh) + 1.f;
     }
-  }
+    wsync();
+  };
 
-  STAMP(t_grad);
   STAMP(t_hess);
   STAMP(t_inv);
   float hrow[R][NUM];  // condensed Hessian rows, swept in place to T = -H^-1 (box path keeps it)
@@ -853,8 +858,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       if (vv[r] < NUM) {
 #pragma unroll
         for (int w = 0; w < NUM; w++) {
-          const int l = w >> 1, bb = w & 1;
-          sm.W[vv[r]][w] = fmaf(C1[r][bb], (float)(kk[r] - l), C0[r][bb]);
+          const int l = w >> 1, bb = w & 1;  // exchange via L: row stride NUM + 1, conflict-free
+          sm.L[vv[r]][w] = fmaf(C1[r][bb], (float)(kk[r] - l), C0[r][bb]);
         }
       }
     }
@@ -864,7 +869,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #pragma unroll
       for (int w = 0; w < NUM; w++) {
         const int l = w >> 1, bb = w & 1;
-        float h = (l <= kk[r]) ? fmaf(C1[r][bb], (float)(kk[r] - l), C0[r][bb]) : sm.W[w][cl[r]];
+        float h = (l <= kk[r]) ? fmaf(C1[r][bb], (float)(kk[r] - l), C0[r][bb]) : sm.L[w][cl[r]];
         if (w == vv[r]) h += ra;
         const bool ok = valid[r] && (w < NU);
         hrow[r][w] = ok ? h : (w == vv[r] ? 1.f : 0.f);
@@ -872,7 +877,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     }
     wsync();
   }
-  if (Hdbg) {  // debug/parity hook: dump H (g was written above), no solve
+  if (Hdbg) {  // debug/parity hook: dump H and g, no solve
+    inputs_and_gradient();
 #pragma unroll
     for (int r = 0; r < R; r++) {
       if (valid[r]) {
@@ -890,7 +896,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   for (int r = 0; r < R; r++) {
     if (vv[r] < NUM) {
 #pragma unroll
-      for (int j = 0; j < NUM; j++) sm.W[vv[r]][j] = -hrow[r][j];  // the sweep leaves -H^-1
+      for (int j = 0; j < NUM; j++) sm.W[j][vv[r]] = -hrow[r][j];  // -H^-1 (symmetric: stored by column, conflict-free)
     }
   }
   wsync();
@@ -913,6 +919,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   }  // !whit
 
   STAMP_SET(t_inv);
+  inputs_and_gradient();
+  STAMP(t_grad);
   // ---- 4. active set -----------------------------------------------------------------------
   float xv[R];           // GI iterate (fp32)
   int actf[R];           // bit t set when constraint 3*v+t is active
@@ -943,12 +951,11 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   // reached in <= 5 passes. The fixed point is then refined in fp64 (residual from the fp64
   // rollout and costate, correction through T on F) and re-checked exactly; a violated row
   // hands the set over to the GI loop below as a valid GI state (independent normals,
-  // positive multipliers). No convergence within kPdasMaxIter passes -> plain GI from the
+  // positive multipliers). No convergence within P.pdas_max passes (10) -> plain GI from the
   // unconstrained point.
   if constexpr (!GAP) {
     if (status == F110QP_SOLVED_ID) {
       STAMP(t_pdas);
-      constexpr int kPdasMaxIter = 10;
       float dg[R], ed[R], gr[R], u[R], lam[R];
       int act[R];  // 0 free, 1 at the lower bound, 2 at the upper bound
 #pragma unroll
@@ -974,7 +981,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         }
       }
       bool converged = false;
-      for (int pit = 0; pit < kPdasMaxIter; pit++) {
+      for (int pit = 0; pit < P.pdas_max; pit++) {
         float y[R], x[R];
 #pragma unroll
         for (int r = 0; r < R; r++)
@@ -1520,8 +1527,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   STAMP(t_end);
   if (lane == 0 && b < 65536) {
     unsigned long long* o = g_stamps + (size_t)b * kStampSlots;
-    o[0] = t_lin - t_start; o[1] = t_grad - t_lin; o[2] = t_hess - t_grad; o[3] = t_inv - t_hess;
-    o[4] = t_gi - t_inv - acc_refine; o[5] = acc_refine; o[6] = t_end - t_gi; o[7] = t_end - t_start;
+    o[0] = t_lin - t_start; o[1] = t_grad - t_inv; o[2] = t_hess - t_lin; o[3] = t_inv - t_hess;
+    o[4] = t_gi - t_grad - acc_refine; o[5] = acc_refine; o[6] = t_end - t_gi; o[7] = t_end - t_start;
     o[8] = acc_s1; o[9] = acc_pdas; o[10] = acc_vj; o[11] = acc_tri; o[12] = acc_z; o[13] = acc_step;
     o[14] = acc_upd; o[15] = it;
     (void)acc_w;
@@ -1548,8 +1555,15 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
                                                    const int* __restrict__ count) {
   __shared__ Smem<NUM, GAP> sm;
   const int n = list ? __builtin_amdgcn_readfirstlane(*count) : B;
+  // XCD-aware order: workgroup i runs on XCD i mod 8, so with one workgroup per QP each XCD
+  // takes a contiguous range of QPs and the 128-B lines of x_ref / u / x are fetched and
+  // written back by one L2 only (a plain order splits every line over 8 L2s).
+  const bool xcd = (list == nullptr) && ((int)gridDim.x == B);
+  const int per = B >> 3, rem = B & 7;
   for (int item = blockIdx.x; item < n; item += gridDim.x) {
-    const int b = list ? __builtin_amdgcn_readfirstlane(list[item]) : item;
+    const int xi = item & 7;
+    const int b = list ? __builtin_amdgcn_readfirstlane(list[item])
+                       : (xcd ? xi * per + (xi < rem ? xi : rem) + (item >> 3) : item);
     solve_qp<NUM, GAP>(sm, b, P, x0g, ulg, xrg, hsg, uout, xout, status_out, iters_out, Hdbg,
                        gdbg, ws);
     wsync();

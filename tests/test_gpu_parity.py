@@ -411,6 +411,17 @@ def test_lane_backend_hands_over_to_wave_kernel(oracle, capi, monkeypatch, be):
     s.close()
 
 
+@pytest.mark.parametrize("cap", ["0", "1", "2"])
+def test_wave_box_pdas_cap_falls_back_to_gi(oracle, capi, monkeypatch, cap):
+    """F110QP_PDAS_MAX caps the wave kernel's box PDAS on the swept Hessian (0: the GI loop
+    solves from the unconstrained point; 1-2: PDAS stops short on the QPs with many active
+    bounds and GI restarts): the results stay exact."""
+    monkeypatch.setenv("F110QP_PDAS_MAX", cap)
+    N = 20
+    w = workload.make_batch(600, N, seed=4242, heading="true", lateral=1.5, steer_range=1.0)
+    check(oracle, capi, N, w, backend=capi.BACKEND_WAVE)
+
+
 def test_lane_and_wave_backends_agree(capi):
     N, B = 20, 4100
     w = workload.make_batch(B, N, seed=1234, heading="true", lateral=1.0)
