@@ -65,15 +65,18 @@ def bytes_per_qp(N: int, gap: bool, warm: bool = False, backend: str = "wave") -
     return inp + out + extra
 
 
-def flops_per_qp(N: int, mean_iters: float, mean_active: float) -> float:
-    """Algorithmic flops of the kernel's algorithm (DESIGN.md "Roofline"):
-    closed-form Hessian 25 n^2, symmetric sweep inverse 2 n^3, x = -W g 2 n^2,
-    per active-set iteration 2 n (W n_p) + 2 q^2 (two triangular solves) + 2 n q (z),
-    two fp64 refinement steps 2 (2 n^2 + 2 q^2 + 2 n q); n = 2N."""
+def flops_per_qp(N: int, passes: float, pivots: float, gap: bool = False) -> float:
+    """Algorithmic flops of the wave kernel (DESIGN.md "Roofline"), n = 2N: closed-form Hessian
+    25 n^2, symmetric sweep inverse 2 n^3; box rows: per PDAS pass one product with the swept
+    matrix T (2 n^2), per bound entering or leaving the free set one pivot of T (2 n^2), two fp64
+    refinement steps (2 n^2 + ~60 n for the fp64 rollout and costate each). Gap rows (GI): per
+    iteration 2 n (W n_p) + 2 q^2 (two triangular solves) + 2 n q (z) with q = pivots."""
     n = 2 * N
-    q = mean_active
-    return 25 * n * n + 2 * n ** 3 + 2 * n * n + mean_iters * (2 * n + 2 * q * q + 2 * n * q) \
-        + 2 * (2 * n * n + 2 * q * q + 2 * n * q)
+    base = 25 * n * n + 2 * n ** 3 + 2 * (2 * n * n + 60 * n)
+    if gap:
+        q = pivots
+        return base + 2 * n * n + passes * (2 * n + 2 * q * q + 2 * n * q)
+    return base + passes * 2 * n * n + pivots * 2 * n * n
 
 
 def load_traffic(config: str, kernel: str):
@@ -332,29 +335,26 @@ def main():
     itn = it.cpu().numpy()
     solved = float((stn == capi.SOLVED).mean())
 
-    # dominant kernel duration: HIP events around single launches on the launch stream
-    evs = []
-    for _ in range(20 if not stream_cfg else 18):
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record(stream)
+    # dominant kernel duration: HIP events on the launch stream around back-to-back launches
+    # (the queue stays full, so host launch overhead is not counted; rocprofv3 --stats agrees)
+    KEV = 20 if not stream_cfg else 18
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    step()
+    a.record(stream)
+    for _ in range(KEV):
         step()
-        b.record(stream)
-        evs.append((a, b))
+    b.record(stream)
     torch.cuda.synchronize(dev)
-    kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))  # ms per launch
+    kms = a.elapsed_time(b) / KEV  # ms per launch
     plan_ms = None
     if tick_cfg:  # the planning kernel alone, same stream
-        pev = []
+        a.record(stream)
         for _ in range(20):
-            a = torch.cuda.Event(enable_timing=True)
-            b = torch.cuda.Event(enable_timing=True)
-            a.record(stream)
             plan_step()
-            b.record(stream)
-            pev.append((a, b))
+        b.record(stream)
         torch.cuda.synchronize(dev)
-        plan_ms = float(np.mean([a.elapsed_time(b) for a, b in pev]))
+        plan_ms = a.elapsed_time(b) / 20
         kms = kms - plan_ms  # the QP kernel(s) of the step
 
     # per-QP latency: single-QP solves (B = 1) through the device entry point (launch + sync)
@@ -377,7 +377,12 @@ def main():
         fpq = LANE_FLOPS_PER_STAGE * N * (float(itn.mean()) + 1.0)
         cpeak, cname = FP64_PEAK_TFLOPS, "fp64_compute"
     else:
-        fpq = flops_per_qp(N, float(itn.mean()), float(itn.mean()))
+        # pivots >= bounds active at the solution (each entered the active set once)
+        un = uo.cpu().numpy()
+        lo = np.float32([cfg.u_min[0], cfg.u_min[1]])
+        hi = np.float32([cfg.u_max[0], cfg.u_max[1]])
+        n_act = float(((np.abs(un - lo) < 1e-6) | (np.abs(un - hi) < 1e-6)).sum(axis=(1, 2)).mean())
+        fpq = flops_per_qp(N, float(itn.mean()), n_act, gap)
         cpeak, cname = FP32_PEAK_TFLOPS, "fp32_compute"
     achieved_gbs = bpq * Bper / (kms * 1e-3) / 1e9
     achieved_tf = fpq * Bper / (kms * 1e-3) / 1e12

@@ -54,12 +54,44 @@ struct DevBuf {
   }
 };
 
+// Pinned, device-visible (fine-grained, coherent) host buffer that only grows.
+struct HostBuf {
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { release(); }
+  void* p = nullptr;  // host address
+  void* d = nullptr;  // device address of the same memory
+  size_t bytes = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= bytes) return hipSuccess;
+    release();
+    hipError_t e = hipHostMalloc(&p, n, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e != hipSuccess) { p = nullptr; return e; }
+    e = hipHostGetDevicePointer(&d, p, 0);
+    if (e != hipSuccess) { release(); return e; }
+    bytes = n;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = d = nullptr;
+    bytes = 0;
+  }
+};
+
+// Host-pointer calls of up to this many QPs (the per-tick call of the host MPC class) let the
+// kernel read its inputs from and write its outputs to the pinned staging buffers directly
+// (zero-copy over PCIe): one launch and one synchronisation per call, no copy engine.
+constexpr int kZeroCopyMaxBatch = 64;
+
 }  // namespace
 
 struct f110qp_ctx {
   f110qp_config cfg;
   f110qp::KParams kp;
-  DevBuf x0, ul, xr, hs, uo, xo, st, it;
+  HostBuf hin, hout;  // host-pointer entry point: packed pinned staging [x0|u_lin|x_ref|hs], [u|x|st|it]
+  DevBuf din, dout;   // their device copies for batches above kZeroCopyMaxBatch
   DevBuf wW, wkey, wact;  // warm-start slot state (config.warm_start)
   int warm_batch = 0;     // batch size the warm state was laid out for
   DevBuf lscr, lfail, lcnt;  // lane back end: Riccati scratch, hand-over list, 2 counters
@@ -158,8 +190,7 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
 
 void f110qp_destroy(f110qp_ctx* c) {
   if (!c) return;
-  c->x0.release(); c->ul.release(); c->xr.release(); c->hs.release();
-  c->uo.release(); c->xo.release(); c->st.release(); c->it.release();
+  c->hin.release(); c->hout.release(); c->din.release(); c->dout.release();
   c->wW.release(); c->wkey.release(); c->wact.release();
   c->lscr.release(); c->lfail.release(); c->lcnt.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -276,16 +307,29 @@ int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* u
   const size_t S = (size_t)c->kp.xr_stride;
   const size_t s_x0 = B * 3 * 4, s_ul = B * 2 * 4, s_xr = B * S * 3 * 4, s_hs = B * 6 * 4;
   const size_t s_uo = B * N * 2 * 4, s_xo = B * (N + 1) * 3 * 4, s_st = B * 4;
-  if ((e = c->x0.ensure(s_x0)) || (e = c->ul.ensure(s_ul)) || (e = c->xr.ensure(s_xr)) ||
-      (gap && (e = c->hs.ensure(s_hs))) || (e = c->uo.ensure(s_uo)) || (e = c->xo.ensure(s_xo)) ||
-      (e = c->st.ensure(s_st)) || (e = c->it.ensure(s_st)))
-    return hip_fail(e, "hipMalloc workspace");
+  // packed layouts (every size a multiple of 4 bytes): in = x0 | u_lin | x_ref | halfspace,
+  // out = u | x | status | iters
+  const size_t o_ul = s_x0, o_xr = o_ul + s_ul, o_hs = o_xr + s_xr, in_bytes = o_hs + (gap ? s_hs : 0);
+  const size_t o_xo = s_uo, o_st = o_xo + s_xo, o_it = o_st + s_st, out_bytes = o_it + s_st;
+  if ((e = c->hin.ensure(in_bytes)) || (e = c->hout.ensure(out_bytes)))
+    return hip_fail(e, "hipHostMalloc staging");
+  char* hi = (char*)c->hin.p;
+  std::memcpy(hi, x0, s_x0);
+  std::memcpy(hi + o_ul, ul, s_ul);
+  std::memcpy(hi + o_xr, xr, s_xr);
+  if (gap) std::memcpy(hi + o_hs, hs, s_hs);
   hipStream_t s = c->stream;
-  if ((e = hipMemcpyAsync(c->x0.p, x0, s_x0, hipMemcpyHostToDevice, s)) ||
-      (e = hipMemcpyAsync(c->ul.p, ul, s_ul, hipMemcpyHostToDevice, s)) ||
-      (e = hipMemcpyAsync(c->xr.p, xr, s_xr, hipMemcpyHostToDevice, s)) ||
-      (gap && (e = hipMemcpyAsync(c->hs.p, hs, s_hs, hipMemcpyHostToDevice, s))))
-    return hip_fail(e, "hipMemcpyAsync H2D");
+  const bool zc = batch <= kZeroCopyMaxBatch;
+  char* di = (char*)c->hin.d;
+  char* dq = (char*)c->hout.d;
+  if (!zc) {
+    if ((e = c->din.ensure(in_bytes)) || (e = c->dout.ensure(out_bytes)))
+      return hip_fail(e, "hipMalloc workspace");
+    di = (char*)c->din.p;
+    dq = (char*)c->dout.p;
+    if ((e = hipMemcpyAsync(di, c->hin.p, in_bytes, hipMemcpyHostToDevice, s)))
+      return hip_fail(e, "hipMemcpyAsync H2D");
+  }
   f110qp::WarmState ws;
   rc = warm_state(c, batch, s, &ws);
   if (rc) return rc;
@@ -293,18 +337,20 @@ int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* u
   f110qp::LaneWork lw;
   rc = lane_work(c, batch, s, &backend, &lw);
   if (rc) return rc;
-  e = f110qp::launch_solve(c->kp, batch, (const float*)c->x0.p, (const float*)c->ul.p,
-                           (const float*)c->xr.p, gap ? (const float*)c->hs.p : nullptr,
-                           (float*)c->uo.p, (float*)c->xo.p, (int*)c->st.p, (int*)c->it.p, ws,
-                           backend, lw, s);
+  e = f110qp::launch_solve(c->kp, batch, (const float*)di, (const float*)(di + o_ul),
+                           (const float*)(di + o_xr), gap ? (const float*)(di + o_hs) : nullptr,
+                           (float*)dq, (float*)(dq + o_xo), (int*)(dq + o_st), (int*)(dq + o_it),
+                           ws, backend, lw, s);
   if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
-  if ((e = hipMemcpyAsync(uo, c->uo.p, s_uo, hipMemcpyDeviceToHost, s)) ||
-      (e = hipMemcpyAsync(xo, c->xo.p, s_xo, hipMemcpyDeviceToHost, s)) ||
-      (e = hipMemcpyAsync(st, c->st.p, s_st, hipMemcpyDeviceToHost, s)) ||
-      (it && (e = hipMemcpyAsync(it, c->it.p, s_st, hipMemcpyDeviceToHost, s))))
+  if (!zc && (e = hipMemcpyAsync(c->hout.p, dq, out_bytes, hipMemcpyDeviceToHost, s)))
     return hip_fail(e, "hipMemcpyAsync D2H");
   e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  const char* ho = (const char*)c->hout.p;
+  std::memcpy(uo, ho, s_uo);
+  std::memcpy(xo, ho + o_xo, s_xo);
+  std::memcpy(st, ho + o_st, s_st);
+  if (it) std::memcpy(it, ho + o_it, s_st);
   return F110QP_OK;
 }
 
