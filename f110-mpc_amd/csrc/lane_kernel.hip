@@ -454,8 +454,13 @@ hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* ul
   // auto: fp64 scratch in LDS while one wave per CU covers the batch (latency), else fp32
   // scratch in the HBM workspace: it halves the scratch traffic that binds large batches, and
   // with the state recentred on x0 the fp32 gains and trajectories stay within ~1e-7 of the
-  // exact optimum (tests/test_gpu_parity.py::test_lane_backend_scratch_modes)
-  if (mode == 0) mode = (lds64 <= cap && (B + 63) / 64 <= 256) ? 1 : 4;
+  // exact optimum (tests/test_gpu_parity.py::test_lane_backend_scratch_modes). Where fp64 does
+  // not fit one wave per CU (N > 24) the fp32 scratch still does: LDS fp32 beats HBM fp32 there
+  // (C4 shard 8,192 x N = 40: 236.5 vs 261.0 us).
+  if (mode == 0) {
+    const bool one_wave_per_cu = (B + 63) / 64 <= 256;
+    mode = one_wave_per_cu && lds64 <= cap ? 1 : one_wave_per_cu && lds32 <= cap ? 2 : 4;
+  }
   if (mode == 1 && lds64 <= cap)
     return launch_lane_t<double, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds64, s);
   if (mode == 2 && lds32 <= cap)

@@ -106,6 +106,87 @@ template <int P, int K> struct SweepHyb {
   static __device__ __forceinline__ void run(float (&h)[NUM], int lane, float* col) { step_hyb<P, K>(h, lane, col); SweepHyb<P + 1, K>::run(h, lane, col); }
 };
 template <int K> struct SweepHyb<NUM, K> { static __device__ __forceinline__ void run(float (&)[NUM], int, float*) {} };
+// ---- E: 2D layout: lane (ga, gb) of an 8 x 8 grid holds the S x S block (ga S.., gb S..) ----
+// Pivot P: the lanes of row block P/S publish their row-P segment (S values, LDS segment stride
+// 8); every lane reads the two segments it needs (its rows' pivot-column entries = row-P entries
+// by symmetry, and its columns' row-P entries) and updates S x S entries.
+constexpr int S2 = NUM / 8;
+template <int P>
+__device__ __forceinline__ void publish_2d(const float (&h)[S2][S2], int ga, int gb, float* prow) {
+  constexpr int aP = P / S2, rP = P % S2;
+  float* pr = prow + (P & 1) * 64;
+  if (ga == aP) {
+#pragma unroll
+    for (int c = 0; c < S2; c++) pr[gb * 8 + c] = h[rP][c];
+  }
+  // the next step's reads must stay after these writes (LDS is in order within a wave; the
+  // fences only stop the compiler from reordering and emit no wait)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// pivot P on the row published by the previous step; row P+1 is updated first and published
+// before the rest of the update, so its LDS round trip overlaps the remaining FMAs
+template <int P>
+__device__ __forceinline__ void step_2d(float (&h)[S2][S2], int ga, int gb, float* prow) {
+  constexpr int aP = P / S2, rP = P % S2;
+  constexpr int P1 = P + 1, rP1 = P1 % S2;
+  const float* pr = prow + (P & 1) * 64;
+  float fr[S2], rk[S2];
+#pragma unroll
+  for (int r = 0; r < S2; r++) fr[r] = pr[ga * 8 + r];
+#pragma unroll
+  for (int c = 0; c < S2; c++) rk[c] = pr[gb * 8 + c];
+  const float inv = __builtin_amdgcn_rcpf(pr[aP * 8 + rP]);
+  float f[S2];
+#pragma unroll
+  for (int r = 0; r < S2; r++) f[r] = fr[r] * inv;
+  f[rP] = (ga == aP) ? 1.f - inv : f[rP];
+  rk[rP] = (gb == aP) ? rk[rP] - 1.f : rk[rP];
+  if constexpr (P1 < NUM) {
+#pragma unroll
+    for (int c = 0; c < S2; c++) h[rP1][c] = fmaf(-f[rP1], rk[c], h[rP1][c]);
+    publish_2d<P1>(h, ga, gb, prow);
+  }
+#pragma unroll
+  for (int r = 0; r < S2; r++) {
+    if (P1 < NUM && r == rP1) continue;
+#pragma unroll
+    for (int c = 0; c < S2; c++) h[r][c] = fmaf(-f[r], rk[c], h[r][c]);
+  }
+  h[rP][rP] = (ga == aP && gb == aP) ? -inv : h[rP][rP];
+}
+template <int P> struct Sweep2D {
+  static __device__ __forceinline__ void run(float (&h)[S2][S2], int ga, int gb, float* pr) { step_2d<P>(h, ga, gb, pr); Sweep2D<P + 1>::run(h, ga, gb, pr); }
+};
+template <> struct Sweep2D<NUM> { static __device__ __forceinline__ void run(float (&)[S2][S2], int, int, float*) {} };
+
+__global__ __launch_bounds__(64) void kern2d(const float* H, float* W, long long* cyc, int reps) {
+  __shared__ __attribute__((aligned(16))) float prow[128];
+  const int lane = threadIdx.x, b = blockIdx.x, ga = lane >> 3, gb = lane & 7;
+  float h[S2][S2], acc = 0.f;
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  for (int rep = 0; rep < reps; rep++) {
+#pragma unroll
+    for (int r = 0; r < S2; r++)
+#pragma unroll
+      for (int c = 0; c < S2; c++) h[r][c] = H[((size_t)b * NUM + ga * S2 + r) * NUM + gb * S2 + c];
+    publish_2d<0>(h, ga, gb, prow);
+    Sweep2D<0>::run(h, ga, gb, prow);
+#pragma unroll
+    for (int r = 0; r < S2; r++)
+#pragma unroll
+      for (int c = 0; c < S2; c++) acc += h[r][c];
+  }
+  asm volatile("" ::"v"(acc));
+  const long long t1 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+  for (int r = 0; r < S2; r++)
+#pragma unroll
+    for (int c = 0; c < S2; c++) W[((size_t)b * NUM + ga * S2 + r) * NUM + gb * S2 + c] = h[r][c];
+  if (lane == 0) cyc[b] = t1 - t0;
+}
+
 template <int P> struct SweepRL {
   static __device__ __forceinline__ void run(float (&h)[NUM], int lane) { step_rl<P>(h, lane); SweepRL<P + 1>::run(h, lane); }
 };
@@ -257,8 +338,8 @@ int main() {
   hipMalloc(&dW, H.size() * 4);
   hipMalloc(&dc, B * 8);
   hipMemcpy(dH, H.data(), H.size() * 4, hipMemcpyHostToDevice);
-  const char* names[12] = {"readlane", "lds", "lds2", "lds-nobar", "lds2-nobar", "rl-scalar", "fma-only", "hyb8", "hyb12", "hyb16", "hyb20", "hyb24"};
-  for (int v = 0; v < 12; v++) {
+  const char* names[13] = {"readlane", "lds", "lds2", "lds-nobar", "lds2-nobar", "rl-scalar", "fma-only", "hyb8", "hyb12", "hyb16", "hyb20", "hyb24", "2d"};
+  for (int v = 0; v < 13; v++) {
     double meanr[2] = {0, 0}, maxr[2] = {0, 0};
     std::vector<float> W(H.size());
     for (int k = 0; k < 2; k++) {
@@ -276,6 +357,7 @@ int main() {
         if (v == 9) hipLaunchKernelGGL(kern<9>, dim3(B), dim3(64), 0, 0, dH, dW, dc, reps);
         if (v == 10) hipLaunchKernelGGL(kern<10>, dim3(B), dim3(64), 0, 0, dH, dW, dc, reps);
         if (v == 11) hipLaunchKernelGGL(kern<11>, dim3(B), dim3(64), 0, 0, dH, dW, dc, reps);
+        if (v == 12) hipLaunchKernelGGL(kern2d, dim3(B), dim3(64), 0, 0, dH, dW, dc, reps);
       }
       hipDeviceSynchronize();
       std::vector<long long> c(B);
