@@ -29,7 +29,7 @@ BACKEND_AUTO = 0
 BACKEND_WAVE = 1
 BACKEND_LANE = 2
 LANE_MIN_BATCH = 4096
-LANE_MIN_BATCH_WIDE = 512
+LANE_MIN_BATCH_WIDE = 1025
 
 
 def auto_backend(horizon: int, batch: int, gap: bool) -> int:

@@ -67,7 +67,7 @@ extern "C" {
 #define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64 (box rows only;     */
                                   /* gap rows always use the wave back end)                   */
 #define F110QP_LANE_MIN_BATCH 4096       /* measured wave/lane crossover on MI355X, N = 20 */
-#define F110QP_LANE_MIN_BATCH_WIDE 512   /* N > 32 (two register rows in the wave kernel)  */
+#define F110QP_LANE_MIN_BATCH_WIDE 1025  /* N > 32: beyond one wave per SIMD (1,024 QPs)   */
 
 #define F110QP_MAX_HORIZON 48  /* 2N <= 96 decision variables: two register rows per lane */
 

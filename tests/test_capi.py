@@ -111,9 +111,9 @@ def test_capi_raises_when_library_missing(monkeypatch):
 
 def test_auto_backend_policy(capi):
     """BACKEND_AUTO: the wave kernel for small box batches and for gap rows, the lane kernel
-    from the measured crossover (4,096 QPs at N <= 32, 512 at N > 32)."""
+    from the measured crossover (4,096 QPs at N <= 32; above 1,024 at N > 32)."""
     assert capi.auto_backend(20, 1024, False) == capi.BACKEND_WAVE
     assert capi.auto_backend(20, 4096, False) == capi.BACKEND_LANE
     assert capi.auto_backend(20, 65536, True) == capi.BACKEND_WAVE
-    assert capi.auto_backend(40, 512, False) == capi.BACKEND_LANE
-    assert capi.auto_backend(40, 256, False) == capi.BACKEND_WAVE
+    assert capi.auto_backend(40, 1025, False) == capi.BACKEND_LANE
+    assert capi.auto_backend(40, 1024, False) == capi.BACKEND_WAVE
