@@ -200,6 +200,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override batch per GPU")
+    ap.add_argument("--horizon", type=int, default=0, help="override the config's horizon N")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -239,6 +240,8 @@ def main():
     Bper, N, gap, warm, desc = CONFIGS[args.config]
     if args.batch:
         Bper = args.batch
+    if args.horizon:
+        N = args.horizon
     strong = args.config in STRONG
     stream_cfg = args.config.startswith("c5")
     tick_cfg = args.config == "tick"
