@@ -209,6 +209,9 @@ def main():
                          "ranks on fewer GPUs (ranks share devices round robin)")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the latency probes (profiling runs: only the config's launches)")
+    ap.add_argument("--grouped", default="auto", choices=["auto", "on", "off"],
+                    help="grouped solve (one W = H^-1 per 120-candidate scenario, f110qp_solve_grouped_dev); "
+                         "auto = on for c4")
     ap.add_argument("--backend", default="auto", choices=["auto", "wave", "lane"],
                     help="solver back end (auto: lane-per-QP for box-only batches >= 2048)")
     args = ap.parse_args()
@@ -267,6 +270,7 @@ def main():
         lo, hi = shard.shard_range(total, world, rank, GROUP)
         g = workload.make_grouped_batch(-(-total // GROUP), N, seed=4000)
         w = {k: np.ascontiguousarray(g[k][:total][lo:hi]) for k in ("x0", "u_lin", "x_ref")}
+        gid_np = (np.arange(lo, hi) // GROUP - lo // GROUP).astype(np.int32)
         Bper = hi - lo
     elif stream_cfg:
         # one tick of the stream per step, all ticks staged in HBM before timing
@@ -294,7 +298,13 @@ def main():
     cfg = capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, device=dev.index,
                               warm_start=int(warm), backend=backend,
                               x_ref_points=(pcfg.traj_discrete if tick_cfg else 0))
-    eff = capi.auto_backend(N, Bper, gap) if backend == capi.BACKEND_AUTO else backend
+    grouped = (args.grouped == "on") or (args.grouped == "auto" and strong)
+    if grouped:
+        if not strong:  # independent ticks: every QP its own group (measures the prepare overhead)
+            gid_np = np.arange(Bper, dtype=np.int32)
+        gid = torch.from_numpy(gid_np).to(dev)
+        ngroups = int(gid_np.max()) + 1
+    eff = capi.auto_backend(N, Bper, gap, grouped) if backend == capi.BACKEND_AUTO else backend
     be_name = "lane" if (eff == capi.BACKEND_LANE and not gap) else "wave"
     solver = capi.Solver(cfg)
     stream = torch.cuda.current_stream(dev)
@@ -314,6 +324,8 @@ def main():
             t = tick[0] % X0.shape[0]  # the latency probe after the timed region wraps around
             tick[0] += 1
             solver.solve_dev(X0[t], UL[t], XR[t], hs, uo, xo, st, it, stream=stream)
+        elif grouped:
+            solver.solve_grouped_dev(x0, ul, xr, hs, gid, ngroups, uo, xo, st, it, stream=stream)
         else:
             solver.solve_dev(x0, ul, xr, hs, uo, xo, st, it, stream=stream)
 
@@ -411,7 +423,8 @@ def main():
             "horizon": N,
             "gap_rows": bool(gap),
             "warm_start": bool(warm),
-            "backend": {"wave": "wave-per-QP (condensed, PDAS/GI)", "lane": "lane-per-QP (Riccati/PDAS fp64)"}[be_name],
+            "backend": {"wave": "wave-per-QP (condensed, PDAS/GI)", "lane": "lane-per-QP (Riccati/PDAS fp64)"}[be_name]
+                       + (" grouped: one W = H^-1 per scenario" if grouped and be_name == "wave" else ""),
             "parallelism": f"independent QP shards x{world} (no collective)"
                            + (f", scenario-aligned ({GROUP}) split of one global batch" if strong else ""),
             "solved_fraction": solved,

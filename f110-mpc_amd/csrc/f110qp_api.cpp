@@ -94,6 +94,8 @@ struct f110qp_ctx {
   DevBuf din, dout;   // their device copies for batches above kZeroCopyMaxBatch
   DevBuf wW, wkey, wact;  // warm-start slot state (config.warm_start)
   int warm_batch = 0;     // batch size the warm state was laid out for
+  DevBuf gW, gkey, glead;    // grouped mode: W = H^-1, key and leader per group
+  DevBuf dgrp;               // host-pointer grouped calls: device copy of the group ids
   DevBuf lscr, lfail, lcnt;  // lane back end: Riccati scratch, hand-over list, 2 counters
   int lane_parity = 0;       // which of the two counters this call appends to
   int lane_kmax = 16;        // PDAS passes of the lane back end before the wave kernel takes over
@@ -193,6 +195,7 @@ void f110qp_destroy(f110qp_ctx* c) {
   c->hin.release(); c->hout.release(); c->din.release(); c->dout.release();
   c->wW.release(); c->wkey.release(); c->wact.release();
   c->lscr.release(); c->lfail.release(); c->lcnt.release();
+  c->gW.release(); c->gkey.release(); c->glead.release(); c->dgrp.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -234,12 +237,15 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
 }
 
 // Back end of a call and, for the lane back end, its workspace.
-static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110qp::LaneWork* lw) {
+static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110qp::LaneWork* lw,
+                     bool grouped = false) {
   *lw = f110qp::LaneWork();
   const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
   int be = c->cfg.backend;
   if (be == F110QP_BACKEND_AUTO) {
-    const int min_b = c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH : F110QP_LANE_MIN_BATCH_WIDE;
+    const int min_b = grouped ? (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH_GROUPED
+                                                      : F110QP_LANE_MIN_BATCH_GROUPED_WIDE)
+                              : (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH : F110QP_LANE_MIN_BATCH_WIDE);
     be = (!gap && batch >= min_b) ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
   }
   if (gap) be = F110QP_BACKEND_WAVE;
@@ -290,9 +296,73 @@ int f110qp_solve_batch_dev(f110qp_ctx* c, int batch, const float* x0, const floa
   return F110QP_OK;
 }
 
+// Per-group W cache of a grouped call (grows only; every call re-fills the slots it uses).
+static int group_state(f110qp_ctx* c, const int* group, int num_groups, f110qp::WarmState* gws,
+                       int** leader) {
+  const size_t G = (size_t)num_groups, nu = 2 * (size_t)c->cfg.horizon;
+  hipError_t e;
+  if ((e = c->gW.ensure(G * nu * nu * 4)) || (e = c->gkey.ensure(G * 16)) || (e = c->glead.ensure(G * 4)))
+    return hip_fail(e, "hipMalloc group state");
+  *gws = f110qp::WarmState();
+  gws->W = (float*)c->gW.p;
+  gws->key = (unsigned*)c->gkey.p;
+  gws->group = group;
+  gws->ngroups = num_groups;
+  *leader = (int*)c->glead.p;
+  return F110QP_OK;
+}
+
+static int check_groups(const int* group, int num_groups, int batch) {
+  if (!group) return fail(F110QP_ERR_INVALID, "group is NULL");
+  (void)batch;
+  if (num_groups < 1 || num_groups > (1 << 22)) return fail(F110QP_ERR_INVALID, "num_groups must be in [1, 2^22]");
+  return F110QP_OK;
+}
+
+int f110qp_solve_grouped_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                             const float* xr, const float* hs, const int* group, int num_groups,
+                             float* uo, float* xo, int* st, int* it, void* stream) {
+  int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
+  if (rc || batch == 0) return rc;
+  if ((rc = check_groups(group, num_groups, batch))) return rc;
+  const float* h = (c->cfg.gap_mode == F110QP_GAP_ACTIVE) ? hs : nullptr;
+  f110qp::WarmState gws;
+  int* leader;
+  if ((rc = group_state(c, group, num_groups, &gws, &leader))) return rc;
+  int backend;
+  f110qp::LaneWork lw;
+  if ((rc = lane_work(c, batch, (hipStream_t)stream, &backend, &lw, true))) return rc;
+  hipError_t e = f110qp::launch_solve_grouped(c->kp, batch, x0, ul, xr, h, uo, xo, st, it, gws,
+                                              leader, backend, lw, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "grouped solve launch");
+  return F110QP_OK;
+}
+
+static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul, const float* xr,
+                      const float* hs, const int* group, int num_groups, float* uo, float* xo,
+                      int* st, int* it);
+
 int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                        const float* xr, const float* hs, float* uo, float* xo, int* st,
                        int* it) {
+  return solve_host(c, batch, x0, ul, xr, hs, nullptr, 0, uo, xo, st, it);
+}
+
+int f110qp_solve_grouped(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                         const float* xr, const float* hs, const int* group, int num_groups,
+                         float* uo, float* xo, int* st, int* it) {
+  if (batch > 0) {
+    const int rc = check_groups(group, num_groups, batch);
+    if (rc) return rc;
+  }
+  return solve_host(c, batch, x0, ul, xr, hs, group, num_groups, uo, xo, st, it);
+}
+
+}  // extern "C"
+
+static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul, const float* xr,
+                      const float* hs, const int* group, int num_groups, float* uo, float* xo,
+                      int* st, int* it) {
   int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
   if (rc || batch == 0) return rc;
   hipError_t e = hipSetDevice(c->cfg.device);
@@ -330,17 +400,28 @@ int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* u
     if ((e = hipMemcpyAsync(di, c->hin.p, in_bytes, hipMemcpyHostToDevice, s)))
       return hip_fail(e, "hipMemcpyAsync H2D");
   }
-  f110qp::WarmState ws;
-  rc = warm_state(c, batch, s, &ws);
-  if (rc) return rc;
   int backend;
   f110qp::LaneWork lw;
-  rc = lane_work(c, batch, s, &backend, &lw);
-  if (rc) return rc;
-  e = f110qp::launch_solve(c->kp, batch, (const float*)di, (const float*)(di + o_ul),
-                           (const float*)(di + o_xr), gap ? (const float*)(di + o_hs) : nullptr,
-                           (float*)dq, (float*)(dq + o_xo), (int*)(dq + o_st), (int*)(dq + o_it),
-                           ws, backend, lw, s);
+  if (group) {
+    if ((e = c->dgrp.ensure(B * 4)) || (e = hipMemcpyAsync(c->dgrp.p, group, B * 4, hipMemcpyHostToDevice, s)))
+      return hip_fail(e, "group ids H2D");
+    f110qp::WarmState gws;
+    int* leader;
+    if ((rc = group_state(c, (const int*)c->dgrp.p, num_groups, &gws, &leader))) return rc;
+    if ((rc = lane_work(c, batch, s, &backend, &lw, true))) return rc;
+    e = f110qp::launch_solve_grouped(c->kp, batch, (const float*)di, (const float*)(di + o_ul),
+                                     (const float*)(di + o_xr), gap ? (const float*)(di + o_hs) : nullptr,
+                                     (float*)dq, (float*)(dq + o_xo), (int*)(dq + o_st),
+                                     (int*)(dq + o_it), gws, leader, backend, lw, s);
+  } else {
+    f110qp::WarmState ws;
+    if ((rc = warm_state(c, batch, s, &ws))) return rc;
+    if ((rc = lane_work(c, batch, s, &backend, &lw))) return rc;
+    e = f110qp::launch_solve(c->kp, batch, (const float*)di, (const float*)(di + o_ul),
+                             (const float*)(di + o_xr), gap ? (const float*)(di + o_hs) : nullptr,
+                             (float*)dq, (float*)(dq + o_xo), (int*)(dq + o_st), (int*)(dq + o_it),
+                             ws, backend, lw, s);
+  }
   if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
   if (!zc && (e = hipMemcpyAsync(c->hout.p, dq, out_bytes, hipMemcpyDeviceToHost, s)))
     return hip_fail(e, "hipMemcpyAsync D2H");
@@ -353,6 +434,8 @@ int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* u
   if (it) std::memcpy(it, ho + o_it, s_st);
   return F110QP_OK;
 }
+
+extern "C" {
 
 int f110qp_condense_debug_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                               const float* xr, double* H, double* g, void* stream) {

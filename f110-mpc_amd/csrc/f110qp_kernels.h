@@ -31,10 +31,17 @@ struct KParams {
 //   act[b] the active bounds at the last solution, per register row r of the lane map
 //          (R = ceil(2N/64) rows): bit lane of act[2(R b + r)] lower, act[2(R b + r) + 1] upper.
 // H depends only on the linearisation point (model.cpp:30-59), so a key hit reuses W exactly.
+// Grouped mode (f110qp_solve_grouped*) reuses W/key as a per-GROUP cache instead: group[b] in
+// [0, ngroups) names QP b's scenario, a prepare launch fills W[g]/key[g] from one member of each
+// group, and every QP whose (theta0, v_lin, delta_lin) bits match its group's key skips the
+// Hessian and the inverse (a QP that does not match builds its own: grouping never changes a
+// result, the group's W is bit-identical to the one the QP would build).
 struct WarmState {
   float* W = nullptr;
   unsigned* key = nullptr;
   unsigned long long* act = nullptr;
+  const int* group = nullptr;
+  int ngroups = 0;
 };
 
 // Workspace of the lane-per-QP kernel (lane_kernel.hip): per-wave Riccati scratch
@@ -62,6 +69,14 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
 hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* u_lin,
                        const float* x_ref, float* u_out, float* x_out, int* status, int* iters,
                        const WarmState& warm, const LaneWork& lw, hipStream_t stream);
+
+// Grouped solve: leader (smallest member) of every group, W = H^-1 per group from its leader,
+// then the solve (wave back end; the lane back end has no factor to share and ignores groups).
+// ws.W/ws.key hold ngroups slots, leader ngroups ints.
+hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const float* u_lin,
+                                const float* x_ref, const float* hs, float* u_out, float* x_out,
+                                int* status, int* iters, const WarmState& gws, int* leader,
+                                int backend, const LaneWork& lw, hipStream_t stream);
 
 // Dump the condensed H (B x 2N x 2N) and g (B x 2N) as built by the solve kernel.
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* u_lin,

@@ -6,23 +6,30 @@
 // model.cpp:30-59, the same at every stage) and the input box rows (mpc.cpp:253,281,290).
 // With the gap rows inactive (the shipped bounds, mpc.cpp:296-300) that is a box-constrained
 // linear-quadratic regulator, and its exact optimum comes from a primal-dual active set on the
-// inputs where every pass is one Riccati recursion over the horizon:
-//   backward  i = N-1..0 : one Riccati step with the stage's fixed inputs masked out (branch
-//                          free): P_i = Hxx + Hux' K_i, p_i = hx + Hux' k_i
-//   forward   i = 0..N-1 : u_i = K_i x_i + k_i, x_{i+1} = A x_i + B u_i + C
-//   adjoint   i = N-1..0 : costate lambda_i = Q(x_i - r_i) + A' lambda_{i+1}; the gradient
-//                          R(u_i - u_des) + B' lambda_{i+1} gives the bound multipliers and
-//                          the PDAS re-guess of stage i (~20 flops per stage)
-// An adjoint sweep that changes nothing certifies the KKT conditions (active bounds with
-// non-negative multipliers, inactive inputs inside the box): the stored forward sweep is the
-// solution. Everything is fp64 in registers (the recursion is ~130 flops per stage), so the
-// result is the exact optimum to ~1e-12, recentred on (x0, y0) like the wave kernel.
+// inputs where every pass is two sweeps over the horizon:
+//   backward i = N-1..0 : one Riccati step with the stage's fixed inputs masked out (branch
+//                         free): K_i, k_i to scratch; P_i = Hxx + Hux' K_i, p_i = hx + Hux' k_i.
+//                         With x_0 = 0 (recentred) the costate at stage 0 is lambda_0 = p_0.
+//   forward  i = 0..N-1 : u_i = K_i x_i + k_i, x_{i+1} = A x_i + B u_i + C, and the costate
+//                         carried FORWARD: lambda_{i+1} = A'^-1 (lambda_i - Q(x_i - r_i)) with
+//                         A'^-1 = I - E' (A = I + E, E^2 = 0, model.cpp:42-46) — the adjoint
+//                         equation lambda_i = Q(x_i - r_i) + A' lambda_{i+1} solved for its
+//                         successor, exact because lambda_i = P_i x_i + p_i on the solution of
+//                         the masked problem. The gradient R(u_i - u_des) + B' lambda_{i+1}
+//                         gives the bound multipliers and the PDAS re-guess of stage i.
+// A forward sweep that changes nothing certifies the KKT conditions (active bounds with
+// non-negative multipliers, inactive inputs inside the box); its u_i (kept in the scratch)
+// roll out to x* in a last output sweep. Everything is fp64 in registers, recentred on
+// (x0, y0, theta0) like the wave kernel, so the result is the exact optimum to ~1e-12 (to
+// ~1e-7 with fp32 scratch).
 //
 // Layout: lane l of workgroup w solves QP b = 64 w + l. The wave's 64 reference paths are
-// contiguous in HBM; they are staged once into LDS transposed ([i][c][lane], conflict free).
-// K_i, k_i (backward -> forward) and u_i, x_i (forward -> next backward) go through a per-wave
-// HBM scratch laid out [stage][8][lane] (fully coalesced 512-B rows, L2 resident at these
-// sizes), the per-stage PDAS state through [stage][lane] ints after it. No cross-lane traffic at all except the wave-uniform "any lane still iterating" vote.
+// contiguous in HBM; they are staged once into LDS transposed ([i][c][lane], conflict free),
+// every load of the wave in flight at once. K_i, k_i (backward -> forward; u_i overwrites
+// K_i's first two slots in the forward) go through a per-wave scratch [stage][8][lane] in LDS
+// while one wave per CU covers the batch, else in an HBM workspace read through a prefetch
+// ring; the per-stage PDAS state sits in LDS. No cross-lane traffic at all except the
+// wave-uniform "any lane still iterating" vote.
 // Lanes that have not converged after kmax passes are appended to a device-side list that the
 // wave-per-QP kernel (solve_kernel.h, GI fallback) then solves.
 #include <hip/hip_runtime.h>
@@ -44,7 +51,7 @@ __device__ unsigned long long g_lstamps[4096 * kLaneStampSlots];
 #define LACC(acc, since)
 #endif
 
-constexpr int kRing = 4;  // stages of scratch loaded ahead in the forward and adjoint sweeps
+constexpr int kRing = 4;  // stages of scratch loaded ahead in the forward and output sweeps
 
 
 // Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
@@ -65,7 +72,7 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
   extern __shared__ __attribute__((aligned(16))) float xr_s[];  // [3N][64] x_ref, transposed
   LSTAMP(t_start);
 #ifdef F110QP_STAMPS
-  unsigned long long acc_bw = 0, acc_fw = 0, acc_adj = 0, acc_out = 0, t_setup = 0, npass = 0;
+  unsigned long long acc_bw = 0, acc_fw = 0, acc_adj = 0, acc_out = 0, t_setup = 0, npass = 0;  // acc_adj: unused (the adjoint is fused into the forward sweep)
 #endif
   const int lane = threadIdx.x;
   const int b0 = blockIdx.x * 64;
@@ -77,30 +84,31 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
 
   // ---- stage the wave's reference paths (nq rows of 3S floats, the first 3N of each used) ---
   // Linear, coalesced sweep over the rows' first 3N entries (element e -> QP e / 3N, entry
-  // e % 3N), eight independent loads in flight per lane, written transposed to LDS.
+  // e % 3N), written transposed to LDS. All loads of a 32-element chunk per lane are issued
+  // before the first LDS write, so the wave waits for HBM once per chunk, not once per load.
   {
     const int S3 = 3 * P.xr_stride;  // floats per QP in x_ref (>= 3N)
     const int nq = (B - b0) < 64 ? (B - b0) : 64;
     const int tot = nq * n3;
     const float* src = xrg + (size_t)b0 * S3;
     const float rn3 = 1.0f / (float)n3;
-    for (int e0 = 0; e0 < tot; e0 += 8 * 64) {
-      float vbuf[8];
-      int qv[8];
+    constexpr int kChunk = 32;
+    for (int e0 = 0; e0 < tot; e0 += kChunk * 64) {
+      float vbuf[kChunk];
+      int dst[kChunk];
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
+      for (int j = 0; j < kChunk; j++) {
         const int e = e0 + j * 64 + lane;
         int q = (int)((float)e * rn3);
         q -= (q * n3 > e) ? 1 : 0;
         q += ((q + 1) * n3 <= e) ? 1 : 0;
-        qv[j] = q;
-        vbuf[j] = (e < tot) ? src[(size_t)q * S3 + (e - q * n3)] : 0.f;
+        const int c = e - q * n3;
+        dst[j] = (e < tot) ? c * 64 + q : -1;
+        vbuf[j] = (e < tot) ? src[(size_t)q * S3 + c] : 0.f;
       }
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int e = e0 + j * 64 + lane;
-        if (e < tot) xr_s[(e - qv[j] * n3) * 64 + qv[j]] = vbuf[j];
-      }
+      for (int j = 0; j < kChunk; j++)
+        if (dst[j] >= 0) xr_s[dst[j]] = vbuf[j];
     }
     __syncthreads();
   }
@@ -130,8 +138,7 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
   const double ub0 = (double)P.umax[0], ub1 = (double)P.umax[1];
 
   // scratch slot (i, e) of this lane: sp[(8 i + e) * 64]; the PDAS state of stage i (2 bits
-  // per input: 0 free, 1 lower bound, 2 upper bound) at ap[i * 64]. Both live in HBM rather
-  // than registers: a per-stage state indexed by the run-time stage would spill anyway.
+  // per input: 0 free, 1 lower bound, 2 upper bound) at ap[i * 64].
   // LDS: [3N][64] references, [N][64] PDAS state, then (SLDS) the [N][8][64] Riccati scratch
   int* ap = reinterpret_cast<int*>(xr_s + 3 * N * 64) + lane;
   ST* sp;
@@ -172,11 +179,7 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
     rt = (double)xr_s[(3 * i + 2) * 64 + lane] - th0;
   };
 
-  // Rounds: a Riccati sweep for the current active set (backward, then forward storing
-  // u_i, x_i), then a light adjoint sweep that re-guesses the set (PDAS). No change certifies
-  // the KKT conditions and the stored forward sweep is the solution.
   bool done = !live;
-  double xN0 = 0.0, xN1 = 0.0, xN2 = 0.0;  // x_N of the last forward sweep
   if (live) {
     // non-finite data -> F110QP_NUMERICAL with NaN outputs (e.g. the planning stage's NaN x_ref
     // of a scenario without a valid candidate, where the reference skips MPC::Update)
@@ -196,6 +199,9 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
 #ifdef F110QP_STAMPS
   t_setup = __builtin_amdgcn_s_memtime() - t_start;
 #endif
+  // Rounds: a Riccati sweep for the current active set (backward), then the forward sweep that
+  // rolls out u_i, x_i and carries the costate to re-guess the set (PDAS). No change certifies
+  // the KKT conditions and the u_i the forward sweep left in the scratch are the solution.
   for (int pass = 0; pass < kmax; pass++) {
     if (__ballot(!done) == 0ull) break;
 #ifdef F110QP_STAMPS
@@ -270,11 +276,13 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
       }
       LACC(acc_bw, t_bw);
       LSTAMP(t_fw);
-      // ---- forward sweep: u_i = K_i x_i + k_i, x_{i+1} = A x_i + B u_i + C --------------
-      // K_i, k_i come through a ring of kRing stages loaded ahead (HBM latency ~ several
-      // stages of compute); the ring index is static inside the unrolled group.
+      // ---- forward sweep: u_i = K_i x_i + k_i, x_{i+1} = A x_i + B u_i + C, costate and the
+      // PDAS re-guess. K_i, k_i come through a ring of kRing stages loaded ahead (HBM latency
+      // ~ several stages of compute); the ring index is static inside the unrolled group.
+      bool changed = false;
       {
         double x0 = 0.0, x1 = 0.0, x2 = 0.0;  // recentred x_0
+        double l0 = p0, l1 = p1, l2 = p2;      // lambda_0 = P_0 x_0 + p_0 = p_0
         ST rg[kRing][8];
 #pragma unroll
         for (int t = 0; t < kRing; t++)
@@ -294,45 +302,15 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
 #pragma unroll
                 for (int e = 0; e < 8; e++) rg[t][e] = s[(kRing * 8 + e) * 64];
               }
-              const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
-              const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
-              s[0] = (ST)u0; s[64] = (ST)u1; s[128] = (ST)x0; s[192] = (ST)x1; s[256] = (ST)x2;
-              const double nx0 = x0 + a02 * x2 + b00 * u0 + c0;
-              const double nx1 = x1 + a12 * x2 + b10 * u0 + c1;
-              const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
-              x0 = nx0; x1 = nx1; x2 = nx2;
-            }
-          }
-        }
-        xN0 = x0; xN1 = x1; xN2 = x2;
-      }
-      LACC(acc_fw, t_fw);
-      LSTAMP(t_adj);
-      // ---- adjoint sweep: bound multipliers and the PDAS re-guess -------------------------
-      bool changed = false;
-      {
-        ref(N - 1, rx, ry, rt);
-        double l0 = q0 * (xN0 - rx), l1 = q1 * (xN1 - ry), l2 = q2 * (xN2 - rt);  // costate
-        ST rg[kRing][5];  // u_i, x_i of the next kRing stages (descending)
-#pragma unroll
-        for (int t = 0; t < kRing; t++)
-          if (t < N) {
-#pragma unroll
-            for (int e = 0; e < 5; e++) rg[t][e] = sp[((size_t)(N - 1 - t) * 8 + e) * 64];
-          }
-        for (int i0 = N - 1; i0 >= 0; i0 -= kRing) {
-#pragma unroll
-          for (int t = 0; t < kRing; t++) {
-            const int i = i0 - t;
-            if (i >= 0) {
-              const double u0 = rg[t][0], u1 = rg[t][1], x0 = rg[t][2], x1 = rg[t][3], x2 = rg[t][4];
-              if (i - kRing >= 0) {
-                const ST* sn = sp + (size_t)(i - kRing) * 8 * 64;
-#pragma unroll
-                for (int e = 0; e < 5; e++) rg[t][e] = sn[e * 64];
-              }
               const int old = ap[i * 64];
               ref(i, rx, ry, rt);
+              const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
+              const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
+              s[0] = (ST)u0; s[64] = (ST)u1;  // the solution if this sweep changes nothing
+              // lambda_{i+1} = (I - E')(lambda_i - Q(x_i - r_i))
+              const double w0 = l0 - q0 * (x0 - rx), w1 = l1 - q1 * (x1 - ry);
+              const double w2 = l2 - q2 * (x2 - rt);
+              l0 = w0; l1 = w1; l2 = w2 - a02 * w0 - a12 * w1;
               // gradient of the objective in u_i: g = R(u - ud) + B' lambda_{i+1}
               const double g0 = r0 * (u0 - ud0) + b00 * l0 + b10 * l1 + b20 * l2;
               const double g1 = r1 * (u1 - ud1) + b21 * l2;
@@ -352,37 +330,51 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                 changed = true;
                 ap[i * 64] = st;
               }
-              // lambda_i = Q(x_i - r_i) + A' lambda_{i+1}  (A = I + E, E only in column 2)
-              const double nl2 = l2 + a02 * l0 + a12 * l1;
-              l0 = q0 * (x0 - rx) + l0;
-              l1 = q1 * (x1 - ry) + l1;
-              l2 = q2 * (x2 - rt) + nl2;
+              const double nx0 = x0 + a02 * x2 + b00 * u0 + c0;
+              const double nx1 = x1 + a12 * x2 + b10 * u0 + c1;
+              const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
+              x0 = nx0; x1 = nx1; x2 = nx2;
             }
           }
         }
       }
-      LACC(acc_adj, t_adj);
+      LACC(acc_fw, t_fw);
       LSTAMP(t_out);
       if (!changed) {
-        // KKT point: write (u*, x*) from the stored forward sweep
+        // KKT point: (u*, x*) from the u_i of this sweep, x* by the same fp64 rollout
         float* uo = uout + (size_t)b * 2 * N;
         float* xo = xout + (size_t)b * 3 * (N + 1);
         xo[0] = x0g[3 * b + 0];  // x*_0 = x0 exactly, as the dynamics rows fix it
         xo[1] = x0g[3 * b + 1];
         xo[2] = fTH0;
-        for (int i = 0; i < N; i++) {
-          const ST* s = sp + (size_t)i * 8 * 64;
-          uo[2 * i] = (float)(double)s[0];
-          uo[2 * i + 1] = (float)(double)s[64];
-          if (i > 0) {
-            xo[3 * i] = (float)((double)s[128] + X0);
-            xo[3 * i + 1] = (float)((double)s[192] + Y0);
-            xo[3 * i + 2] = (float)((double)s[256] + th0);
+        double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+        ST ur[kRing][2];
+#pragma unroll
+        for (int t = 0; t < kRing; t++)
+          if (t < N) { ur[t][0] = sp[(size_t)t * 8 * 64]; ur[t][1] = sp[(size_t)t * 8 * 64 + 64]; }
+        for (int i0 = 0; i0 < N; i0 += kRing) {
+#pragma unroll
+          for (int t = 0; t < kRing; t++) {
+            const int i = i0 + t;
+            if (i < N) {
+              const double u0 = (double)ur[t][0], u1 = (double)ur[t][1];
+              if (i + kRing < N) {
+                const ST* s = sp + (size_t)(i + kRing) * 8 * 64;
+                ur[t][0] = s[0];
+                ur[t][1] = s[64];
+              }
+              uo[2 * i] = (float)u0;
+              uo[2 * i + 1] = (float)u1;
+              const double nx0 = x0 + a02 * x2 + b00 * u0 + c0;
+              const double nx1 = x1 + a12 * x2 + b10 * u0 + c1;
+              const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
+              x0 = nx0; x1 = nx1; x2 = nx2;
+              xo[3 * i + 3] = (float)(x0 + X0);
+              xo[3 * i + 4] = (float)(x1 + Y0);
+              xo[3 * i + 5] = (float)(x2 + th0);
+            }
           }
         }
-        xo[3 * N] = (float)(xN0 + X0);
-        xo[3 * N + 1] = (float)(xN1 + Y0);
-        xo[3 * N + 2] = (float)(xN2 + th0);
         status_out[b] = F110QP_SOLVED_ID;
         if (iters_out) iters_out[b] = pass;  // active-set changes before the KKT point
         done = true;

@@ -9,7 +9,10 @@
   template hipError_t f110qp::launch_t<NUM, GAP>(                                              \
       const KParams&, int, const float*, const float*, const float*, const float*, float*,      \
       float*, int*, int*, double*, double*, const WarmState&, const int*, const int*, int,       \
-      hipStream_t);
+      hipStream_t);                                                                            \
+  template hipError_t f110qp::launch_prep_t<NUM, GAP>(const KParams&, int, const float*,       \
+                                                      const float*, const float*, const float*,  \
+                                                      const WarmState&, const int*, hipStream_t);
 
 #ifdef F110QP_ALL_INST
 #define F110QP_BOTH(NUM) F110QP_INSTANTIATE(NUM, false) F110QP_INSTANTIATE(NUM, true)

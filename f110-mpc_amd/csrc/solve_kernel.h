@@ -679,7 +679,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
                                          int* __restrict__ iters_out,
                                          double* __restrict__ Hdbg,
                                          double* __restrict__ gdbg,
-                                         const WarmState& ws) {
+                                         const WarmState& ws, const int prep_slot = -1) {
   constexpr int R = (NUM + 63) / 64;
   const int lane = threadIdx.x;
   const int N = P.N;
@@ -749,15 +749,25 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   }
   wsync();
 
-  // warm start: does the cached W of this slot belong to the same linearisation point?
+  // W cache: per slot b (warm start), per group (grouped mode), or the group slot a prepare
+  // launch fills (prep_slot >= 0). Does the cached W belong to this linearisation point?
   const bool warm = ws.W != nullptr && Hdbg == nullptr;
+  const bool grp = ws.group != nullptr;
+  const bool prep = prep_slot >= 0;
+  int wslot = b;
+  if (grp) {
+    const int g = __builtin_amdgcn_readfirstlane(ws.group[b]);
+    wslot = (g >= 0 && g < ws.ngroups) ? g : -1;
+  }
+  if (prep) wslot = prep_slot;
   bool whit = false, wvalid = false;
-  if (warm) {
-    const unsigned* key = ws.key + 4 * b;
+  if (warm && !prep && wslot >= 0) {
+    const unsigned* key = ws.key + 4 * wslot;
     wvalid = key[3] == 1u;
     whit = wvalid && key[0] == __float_as_uint(fTH0) && key[1] == __float_as_uint(ul0) &&
            key[2] == __float_as_uint(ul1);
   }
+  const bool seed_act = ws.act != nullptr && !grp && wvalid;  // previous tick's set (warm start)
   STAMP(t_lin);
   // ---- 2a. (run after the inverse) non-finite check, recentred references, gradient at u = 0
   // by the fp64 adjoint, and the free response of the gap rows
@@ -804,8 +814,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   STAMP(t_inv);
   float hrow[R][NUM];  // condensed Hessian rows, swept in place to T = -H^-1 (box path keeps it)
   if (whit) {
-    // ---- 2b/3 (warm hit): W from the slot cache, no Hessian, no sweep ------------------
-    const float* Wc = ws.W + (size_t)b * NU * NU;
+    // ---- 2b/3 (cache hit): W from the slot / group cache, no Hessian, no sweep ----------
+    const float* Wc = ws.W + (size_t)wslot * NU * NU;
 #pragma unroll
     for (int r = 0; r < R; r++) {
       if (vv[r] >= NUM) continue;
@@ -900,15 +910,15 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     }
   }
   wsync();
-  if (warm) {  // prime the slot cache (coalesced: lane v writes column v of every row)
-    float* Wc = ws.W + (size_t)b * NU * NU;
+  if (warm && wslot >= 0 && (prep || !grp)) {  // prime the slot / group cache (coalesced:
+    float* Wc = ws.W + (size_t)wslot * NU * NU;        // lane v writes column v of every row)
     for (int j = 0; j < NU; j++) {
 #pragma unroll
       for (int r = 0; r < R; r++)
         if (valid[r]) Wc[(size_t)j * NU + vv[r]] = sm.W[j][cl[r]];
     }
     if (lane == 0) {
-      unsigned* key = ws.key + 4 * b;
+      unsigned* key = ws.key + 4 * wslot;
       key[0] = __float_as_uint(fTH0);
       key[1] = __float_as_uint(ulg[2 * b + 0]);
       key[2] = __float_as_uint(ulg[2 * b + 1]);
@@ -916,6 +926,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     }
   }
   wsync();
+  if (prep) return;  // prepare launch: the group's W is published, no solve
   }  // !whit
 
   STAMP_SET(t_inv);
@@ -966,7 +977,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         u[r] = 0.f;
         lam[r] = 0.f;
         act[r] = 0;
-        if (warm && wvalid && valid[r]) {  // previous tick's active bounds seed the first guess
+        if (seed_act && valid[r]) {  // previous tick's active bounds seed the first guess
           const unsigned long long lo_m = ws.act[2 * (R * b + r)], hi_m = ws.act[2 * (R * b + r) + 1];
           act[r] = ((lo_m >> lane) & 1ull) ? 1 : (((hi_m >> lane) & 1ull) ? 2 : 0);
         }
@@ -1512,7 +1523,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     status_out[b] = status;
     if (iters_out) iters_out[b] = it;
   }
-  if (warm) {
+  if (ws.act != nullptr && !grp && Hdbg == nullptr) {
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const unsigned long long lo_m = __ballot(ok && valid[r] && (actf[r] & 1));
@@ -1570,6 +1581,29 @@ __global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
   }
 }
 
+// Grouped mode, prepare launch: one wave per group builds the closed-form Hessian and the swept
+// inverse of the group's leader (the smallest member index; none -> the slot is marked empty)
+// and publishes W and the key of its linearisation point (theta0, v, delta) to the group slot.
+template <int NUM, bool GAP>
+__global__ __launch_bounds__(64) void group_prep_kernel(const KParams P, const int G,
+                                                        const float* __restrict__ x0g,
+                                                        const float* __restrict__ ulg,
+                                                        const float* __restrict__ xrg,
+                                                        const float* __restrict__ hsg,
+                                                        const WarmState ws,
+                                                        const int* __restrict__ leader,
+                                                        const int B) {
+  __shared__ Smem<NUM, GAP> sm;
+  const int g = blockIdx.x;
+  const int b = __builtin_amdgcn_readfirstlane(leader[g]);
+  if (b < 0 || b >= B) {
+    if (threadIdx.x == 0) ws.key[4 * g + 3] = 0u;
+    return;
+  }
+  solve_qp<NUM, GAP>(sm, b, P, x0g, ulg, xrg, hsg, nullptr, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, ws, g);
+}
+
 // ------------------------------------------------------------------------------------------
 // launch of one instantiation
 // ------------------------------------------------------------------------------------------
@@ -1580,6 +1614,16 @@ hipError_t launch_t(const KParams& P, int B, const float* x0, const float* ul, c
                     hipStream_t s) {
   hipLaunchKernelGGL((solve_kernel<NUM, GAP>), dim3(grid), dim3(64), 0, s, P, B, x0, ul, xr, hs,
                      uo, xo, st, its, Hd, gd, ws, list, count);
+  return hipGetLastError();
+}
+
+template <int NUM, bool GAP>
+hipError_t launch_prep_t(const KParams& P, int B, const float* x0, const float* ul,
+                         const float* xr, const float* hs, const WarmState& ws, const int* leader,
+                         hipStream_t s) {
+  if (ws.ngroups <= 0) return hipSuccess;
+  hipLaunchKernelGGL((group_prep_kernel<NUM, GAP>), dim3(ws.ngroups), dim3(64), 0, s, P,
+                     ws.ngroups, x0, ul, xr, hs, ws, leader, B);
   return hipGetLastError();
 }
 

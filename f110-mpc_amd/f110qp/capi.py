@@ -30,11 +30,16 @@ BACKEND_WAVE = 1
 BACKEND_LANE = 2
 LANE_MIN_BATCH = 4096
 LANE_MIN_BATCH_WIDE = 1025
+LANE_MIN_BATCH_GROUPED = 16384
+LANE_MIN_BATCH_GROUPED_WIDE = 16384
 
 
-def auto_backend(horizon: int, batch: int, gap: bool) -> int:
+def auto_backend(horizon: int, batch: int, gap: bool, grouped: bool = False) -> int:
     """The back end BACKEND_AUTO resolves to (mirrors lane_work() in f110qp_api.cpp)."""
-    min_b = LANE_MIN_BATCH if horizon <= 32 else LANE_MIN_BATCH_WIDE
+    if grouped:
+        min_b = LANE_MIN_BATCH_GROUPED if horizon <= 32 else LANE_MIN_BATCH_GROUPED_WIDE
+    else:
+        min_b = LANE_MIN_BATCH if horizon <= 32 else LANE_MIN_BATCH_WIDE
     return BACKEND_LANE if (not gap and batch >= min_b) else BACKEND_WAVE
 MAX_HORIZON = 48
 
@@ -47,6 +52,8 @@ EXPORTED = (
     "f110qp_destroy",
     "f110qp_solve_batch",
     "f110qp_solve_batch_dev",
+    "f110qp_solve_grouped",
+    "f110qp_solve_grouped_dev",
     "f110qp_condense_debug_dev",
     "f110qp_warm_reset",
     "f110qp_find_half_spaces",
@@ -114,6 +121,8 @@ def load():
     L.f110qp_destroy.argtypes = [C.c_void_p]
     L.f110qp_solve_batch.argtypes = [C.c_void_p, C.c_int] + [fp] * 8
     L.f110qp_solve_batch_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 9
+    L.f110qp_solve_grouped.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 4
+    L.f110qp_solve_grouped_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 5
     L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
     L.f110qp_warm_reset.argtypes = [C.c_void_p]
     L.f110qp_find_half_spaces.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_float), C.c_int,
@@ -215,6 +224,38 @@ class Solver:
         _check(self.lib.f110qp_solve_batch_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
                                                _tp(u_out), _tp(x_out), _tp(status), _tp(iters),
                                                C.c_void_p(stream.cuda_stream)), "f110qp_solve_batch_dev")
+
+    def solve_grouped(self, x0, u_lin, x_ref, group, num_groups=None, halfspace=None):
+        """Grouped solve on host arrays (f110qp_solve_grouped): group [B] int scenario ids."""
+        N = self.horizon
+        x0 = np.ascontiguousarray(x0, np.float32).reshape(-1, 3)
+        B = x0.shape[0]
+        ul = np.ascontiguousarray(u_lin, np.float32).reshape(B, 2)
+        S = self.config.x_ref_points or N
+        xr = np.ascontiguousarray(x_ref, np.float32).reshape(B, S, 3)
+        hs = None if halfspace is None else np.ascontiguousarray(halfspace, np.float32).reshape(B, 6)
+        g = np.ascontiguousarray(group, np.int32).reshape(B)
+        G = int(g.max()) + 1 if num_groups is None else int(num_groups)
+        u = np.empty((B, N, 2), np.float32)
+        x = np.empty((B, N + 1, 3), np.float32)
+        st = np.empty(B, np.int32)
+        it = np.empty(B, np.int32)
+        _check(self.lib.f110qp_solve_grouped(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(g), G, _p(u), _p(x),
+                                             _p(st), _p(it)), "f110qp_solve_grouped")
+        return u, x, st, it
+
+    def solve_grouped_dev(self, x0, u_lin, x_ref, halfspace, group, num_groups, u_out, x_out, status, iters=None,
+                          stream=None):
+        """Grouped solve on device (torch) tensors; group [B] int32 on the device."""
+        import torch
+
+        B = x0.shape[0]
+        if stream is None:
+            stream = torch.cuda.current_stream(x0.device)
+        _check(self.lib.f110qp_solve_grouped_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
+                                                 _tp(group), int(num_groups), _tp(u_out), _tp(x_out), _tp(status),
+                                                 _tp(iters), C.c_void_p(stream.cuda_stream)),
+               "f110qp_solve_grouped_dev")
 
     def warm_reset(self):
         _check(self.lib.f110qp_warm_reset(self._h), "f110qp_warm_reset")

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define F110QP_API_VERSION 3
+#define F110QP_API_VERSION 4
 
 /* return codes */
 #define F110QP_OK 0
@@ -68,6 +68,10 @@ extern "C" {
                                   /* gap rows always use the wave back end)                   */
 #define F110QP_LANE_MIN_BATCH 4096       /* measured wave/lane crossover on MI355X, N = 20 */
 #define F110QP_LANE_MIN_BATCH_WIDE 1025  /* N > 32: beyond one wave per SIMD (1,024 QPs)   */
+/* grouped calls (f110qp_solve_grouped*): the wave back end reuses one W = H^-1 per group, so it
+ * stays ahead of the lane back end up to these batch sizes (measured) */
+#define F110QP_LANE_MIN_BATCH_GROUPED 16384
+#define F110QP_LANE_MIN_BATCH_GROUPED_WIDE 16384
 
 #define F110QP_MAX_HORIZON 48  /* 2N <= 96 decision variables: two register rows per lane */
 
@@ -121,6 +125,25 @@ int f110qp_solve_batch(f110qp_ctx* ctx, int batch, const float* x0, const float*
 int f110qp_solve_batch_dev(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
                            const float* x_ref, const float* halfspace, float* u_out,
                            float* x_out, int* status, int* iters, void* stream);
+
+/* Grouped solve: the candidates of one control tick share their linearisation point.
+ * Model::Linearize depends only on (theta0, v, delta) (src/model.cpp:30-59), so the candidate
+ * mini-paths of one pose (src/project.cpp:76-113) share A, B, C, the condensed Hessian H and
+ * W = H^-1: only the gradient differs (the proposal's `group` argument, 8(b)).
+ *   group [B]   scenario id of each QP in [0, num_groups); ids need not be contiguous or sorted.
+ * One W per group is built from its first member; every member whose (x0[b][2], u_lin[b]) bits
+ * equal that member's reuses it, any other QP (or an id outside [0, num_groups)) builds its own.
+ * Grouping therefore never changes a result: the output is bit-identical to
+ * f110qp_solve_batch[_dev] on the wave back end. The lane back end (chosen by AUTO above
+ * F110QP_LANE_MIN_BATCH_GROUPED[_WIDE]) factors per QP and ignores the groups. Grouped calls
+ * neither use nor update the warm-start state. Same layouts and conventions as above. */
+int f110qp_solve_grouped(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                         const float* x_ref, const float* halfspace, const int* group,
+                         int num_groups, float* u_out, float* x_out, int* status, int* iters);
+int f110qp_solve_grouped_dev(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                             const float* x_ref, const float* halfspace, const int* group,
+                             int num_groups, float* u_out, float* x_out, int* status, int* iters,
+                             void* stream);
 
 /* Forget the warm-start state of every slot (the next call solves cold). */
 int f110qp_warm_reset(f110qp_ctx* ctx);

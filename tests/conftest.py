@@ -25,6 +25,14 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def capi():
+    # torch ships its own HIP runtime next to the system one libf110qp.so links: the runtime that
+    # initialises first owns the device, and torch's only comes up if it is first
+    try:
+        import torch
+
+        torch.cuda.is_available()
+    except ImportError:
+        pass
     from f110qp import capi as c
 
     c.load()
