@@ -96,10 +96,10 @@ struct f110qp_ctx {
   int warm_batch = 0;     // batch size the warm state was laid out for
   DevBuf gW, gkey, glead;    // grouped mode: W = H^-1, key and leader per group
   DevBuf dgrp;               // host-pointer grouped calls: device copy of the group ids
-  DevBuf lscr, lfail, lcnt;  // lane back end: Riccati scratch, hand-over list, 2 counters
-  int lane_parity = 0;       // which of the two counters this call appends to
-  int lane_kmax = 16;        // PDAS passes of the lane back end before the wave kernel takes over
+  DevBuf lscr;               // lane back end: HBM Riccati scratch (when not in LDS)
+  int lane_kmax = 16;        // lane back end: PDAS passes before single (least-index) flips
   int lane_mode = 0;         // lane scratch placement (LaneWork::mode)
+  int lane_qpw = 0;          // lane QPs per wave (LaneWork::qpw, 0 = auto)
   hipStream_t stream = nullptr;
 };
 
@@ -167,10 +167,16 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     k.umin[i] = cfg->u_min[i];
     k.umax[i] = cfg->u_max[i];
   }
-  // test hook: F110QP_LANE_KMAX forces early hand-over from the lane to the wave back end
+  // test hook: F110QP_LANE_KMAX = PDAS passes of the lane back end before it switches to single
+  // least-index flips (0: single flips from the first pass)
   if (const char* ek = std::getenv("F110QP_LANE_KMAX")) {
     const int v = std::atoi(ek);
-    if (v >= 1 && v <= 64) c->lane_kmax = v;
+    if (v >= 0 && v <= 64) c->lane_kmax = v;
+  }
+  // bench hook: F110QP_LANE_QPW = QPs per wave of the lane back end (power of two <= 64)
+  if (const char* eq = std::getenv("F110QP_LANE_QPW")) {
+    const int v = std::atoi(eq);
+    if (v >= 1 && v <= 64 && (v & (v - 1)) == 0) c->lane_qpw = v;
   }
   // test/bench hook: F110QP_LANE_MODE = 1 LDS fp64, 2 LDS fp32, 3 HBM fp64, 4 HBM fp32 scratch
   if (const char* em = std::getenv("F110QP_LANE_MODE")) {
@@ -194,7 +200,7 @@ void f110qp_destroy(f110qp_ctx* c) {
   if (!c) return;
   c->hin.release(); c->hout.release(); c->din.release(); c->dout.release();
   c->wW.release(); c->wkey.release(); c->wact.release();
-  c->lscr.release(); c->lfail.release(); c->lcnt.release();
+  c->lscr.release();
   c->gW.release(); c->gkey.release(); c->glead.release(); c->dgrp.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -251,23 +257,15 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   if (gap) be = F110QP_BACKEND_WAVE;
   *backend = (be == F110QP_BACKEND_LANE) ? f110qp::BACKEND_LANE : f110qp::BACKEND_WAVE;
   if (*backend == f110qp::BACKEND_WAVE) return F110QP_OK;
-  const size_t waves = ((size_t)batch + 63) / 64, N = (size_t)c->cfg.horizon;
-  hipError_t e;
-  if ((e = c->lscr.ensure(waves * N * 64 * (8 * sizeof(double) + sizeof(int)))) ||
-      (e = c->lfail.ensure((size_t)batch * sizeof(int))))
-    return hip_fail(e, "hipMalloc lane workspace");
-  if (!c->lcnt.p) {
-    if ((e = c->lcnt.ensure(2 * sizeof(int))) || (e = hipMemsetAsync(c->lcnt.p, 0, 2 * sizeof(int), s)))
-      return hip_fail(e, "hipMalloc lane counters");
-  }
-  int* cnt = (int*)c->lcnt.p;
+  // HBM scratch of ceil(B/L) waves x N stages x 8 values x L lanes (<= (B + 63) x N x 8 doubles)
+  (void)s;
+  const size_t N = (size_t)c->cfg.horizon;
+  hipError_t e = c->lscr.ensure(((size_t)batch + 63) * N * 8 * sizeof(double));
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc lane workspace");
   lw->scratch = (double*)c->lscr.p;
-  lw->fail_list = (int*)c->lfail.p;
-  lw->fail_count = cnt + c->lane_parity;
-  lw->fail_count_next = cnt + (1 - c->lane_parity);
   lw->kmax = c->lane_kmax;
   lw->mode = c->lane_mode;
-  c->lane_parity ^= 1;
+  lw->qpw = c->lane_qpw;
   return F110QP_OK;
 }
 

@@ -44,22 +44,23 @@ struct WarmState {
   int ngroups = 0;
 };
 
-// Workspace of the lane-per-QP kernel (lane_kernel.hip): per-wave Riccati scratch
-// (ceil(B/64) x N x 8 x 64 doubles, then ceil(B/64) x N x 64 ints of PDAS state), the device-side list of QPs handed to the wave kernel and
-// two list counters used alternately by consecutive calls (each call clears the other one).
+// Workspace of the lane-per-QP kernel (lane_kernel.hip): the HBM Riccati scratch when it does
+// not stay in LDS (ceil(B/L) x N x 8 x L doubles at most, L QPs per wave <= 64).
 struct LaneWork {
   double* scratch = nullptr;
-  int* fail_list = nullptr;
-  int* fail_count = nullptr;
-  int* fail_count_next = nullptr;
-  int kmax = 16;  // PDAS passes before a QP is handed over
+  int kmax = 16;  // PDAS passes (all violations flip) before single flips (least index)
   int mode = 0;   // scratch: 0 auto, 1 LDS fp64, 2 LDS fp32, 3 HBM fp64, 4 HBM fp32 (workspace)
+  int qpw = 0;    // QPs per wave: 0 auto (lane_qps_per_wave), else a power of two <= 64
 };
+
+// waves the lane kernel's grid aims for (one per CU of the MI355X's 256)
+constexpr int kLaneTargetWaves = 256;
+int lane_qps_per_wave(int B, int qpw);
 
 enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
 
 // Solve B QPs. hs == nullptr -> box-only kernels (gap rows inactive). backend LANE (box rows
-// only): lane-per-QP Riccati/PDAS kernel, then the wave kernel on its non-converged QPs.
+// only): the lane-per-QP Riccati/PDAS kernel alone (one launch, no hand-over).
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u_lin,
                         const float* x_ref, const float* hs, float* u_out, float* x_out,
                         int* status, int* iters, const WarmState& warm, int backend,

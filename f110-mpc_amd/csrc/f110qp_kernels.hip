@@ -43,15 +43,7 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
   if (hs)
     return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
                           nullptr, B, s);
-  if (backend == BACKEND_LANE) {
-    hipError_t e = launch_lane(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
-    if (e != hipSuccess) return e;
-    // the QPs whose PDAS did not settle within kmax passes: wave kernel (GI), grid-stride
-    // over the device-side list (an empty list costs one short launch)
-    const int grid = B < 256 ? B : 256;
-    return launch_g<false>(P, B, x0, ul, xr, nullptr, uo, xo, st, its, nullptr, nullptr, ws,
-                           lw.fail_list, lw.fail_count, grid, s);
-  }
+  if (backend == BACKEND_LANE) return launch_lane(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
   return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
                          nullptr, B, s);
 }

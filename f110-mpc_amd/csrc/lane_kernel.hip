@@ -1,4 +1,4 @@
-// lane_kernel.hip — the throughput path: ONE LANE PER QP (64 box-constrained QPs per wave).
+// lane_kernel.hip — the throughput path: ONE LANE PER QP (up to 64 box-constrained QPs per wave).
 //
 // The reference solves, per control tick, the sparse QP of MPC::Update (src/mpc.cpp:69-143):
 // min sum_i 1/2 |x_i - r_i|_Q^2 + 1/2 |u_i - u_des|_R^2 subject to the dynamics rows
@@ -23,15 +23,30 @@
 // (x0, y0, theta0) like the wave kernel, so the result is the exact optimum to ~1e-12 (to
 // ~1e-7 with fp32 scratch).
 //
-// Layout: lane l of workgroup w solves QP b = 64 w + l. The wave's 64 reference paths are
-// contiguous in HBM; they are staged once into LDS transposed ([i][c][lane], conflict free),
-// every load of the wave in flight at once. K_i, k_i (backward -> forward; u_i overwrites
-// K_i's first two slots in the forward) go through a per-wave scratch [stage][8][lane] in LDS
-// while one wave per CU covers the batch, else in an HBM workspace read through a prefetch
-// ring; the per-stage PDAS state sits in LDS. No cross-lane traffic at all except the
-// wave-uniform "any lane still iterating" vote.
-// Lanes that have not converged after kmax passes are appended to a device-side list that the
-// wave-per-QP kernel (solve_kernel.h, GI fallback) then solves.
+// Layout: a wave solves L QPs (L = 1..64, a power of two): lane l of workgroup w works on QP
+// b = L w + (l mod L), so for L < 64 every QP is computed by 64 / L lanes in lock step; only
+// the first (the owner) stores results. Keeping EXEC full is deliberate: on gfx950 a wave whose
+// EXEC mask is partial runs ~2.4x slower once its CU hosts one wave per SIMD, while full waves
+// do not (tools/microbench/contention.hip) — the same reason a lane whose
+// QP has converged keeps sweeping (its sweeps reproduce the same K, u and set: idempotent)
+// until the whole wave is done, and why the output sweep runs once for all lanes at the end.
+// The duplicates write the same values to the same LDS/HBM slots as their owner (measured free).
+// A wave's time is its slowest QP's passes times the cost of one sweep at one wave per SIMD, so
+// L is the smallest power of two that fits the batch in <= 256 waves (one per CU; measured
+// faster than one per SIMD at 1,024 - 8,192 QPs, and a second wave on a SIMD halves both, the
+// fp64 pipe being saturated by one): small batches spread over the whole chip and each wave
+// waits for the maximum pass count of fewer QPs. The wave's L
+// reference paths are contiguous in HBM; they are staged once into LDS transposed ([i][c][L],
+// conflict free), every load of the wave in flight at once. K_i, k_i (backward -> forward; u_i
+// overwrites K_i's first two slots in the forward) go through a per-wave scratch [stage][8][L]
+// in LDS when the resident waves fit, else in an HBM workspace read through a prefetch ring;
+// the per-stage PDAS state sits in LDS. No cross-lane traffic at all except the wave-uniform
+// "any lane still iterating" vote.
+// Convergence: PDAS (every violated complementarity condition flips at once) for kmax passes;
+// a lane still changing after that flips only its FIRST violation per pass (stage-major,
+// input-minor order: the least-index single principal pivoting of Murty / Bard, finite for
+// box-constrained QPs with a positive definite Hessian, Judice & Pires 1989), so every QP is
+// solved inside this one launch; P.max_iter passes bound it (status MAX_ITER, NaN outputs).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -51,12 +66,15 @@ __device__ unsigned long long g_lstamps[4096 * kLaneStampSlots];
 #define LACC(acc, since)
 #endif
 
-constexpr int kRing = 4;  // stages of scratch loaded ahead in the forward and output sweeps
+// stages of scratch loaded ahead in the forward and output sweeps: HBM latency is several
+// stages of compute, LDS latency (~60 cycles at one wave per SIMD) less than one
+template <bool SLDS>
+constexpr int ring_depth() { return SLDS ? 2 : 4; }
 
 
 // Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
 template <typename ST, bool SLDS>
-__global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
+__global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B, const int L,
                                                   const float* __restrict__ x0g,
                                                   const float* __restrict__ ulg,
                                                   const float* __restrict__ xrg,
@@ -65,34 +83,35 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                                                   int* __restrict__ status_out,
                                                   int* __restrict__ iters_out,
                                                   double* __restrict__ scr,
-                                                  int* __restrict__ fail_list,
-                                                  int* __restrict__ fail_count,
-                                                  int* __restrict__ fail_count_next,
                                                   const WarmState ws, const int kmax) {
-  extern __shared__ __attribute__((aligned(16))) float xr_s[];  // [3N][64] x_ref, transposed
+  extern __shared__ __attribute__((aligned(16))) float xr_s[];  // [3N][L] x_ref, transposed
   LSTAMP(t_start);
 #ifdef F110QP_STAMPS
-  unsigned long long acc_bw = 0, acc_fw = 0, acc_adj = 0, acc_out = 0, t_setup = 0, npass = 0;  // acc_adj: unused (the adjoint is fused into the forward sweep)
+  unsigned long long acc_bw = 0, acc_fw = 0, acc_out = 0, t_setup = 0, npass = 0;
 #endif
+  constexpr int kRing = ring_depth<SLDS>();
   const int lane = threadIdx.x;
-  const int b0 = blockIdx.x * 64;
-  const int b = b0 + lane;
-  const bool live = b < B;
+  const int b0 = blockIdx.x * L;
+  const int nq = (B - b0) < L ? (B - b0) : L;  // QPs of this wave (>= 1)
+  int slot = lane & (L - 1);
+  if (slot >= nq) slot = 0;                     // duplicate of a QP that exists
+  const bool owner = lane < nq;                 // stores the results of QP b
+  const int b = b0 + slot;
   const int N = P.N;
   const int n3 = 3 * N;
-  if (blockIdx.x == 0 && lane == 0) *fail_count_next = 0;  // the next call's list (double buffer)
 
   // ---- stage the wave's reference paths (nq rows of 3S floats, the first 3N of each used) ---
   // Linear, coalesced sweep over the rows' first 3N entries (element e -> QP e / 3N, entry
-  // e % 3N), written transposed to LDS. All loads of a 32-element chunk per lane are issued
-  // before the first LDS write, so the wave waits for HBM once per chunk, not once per load.
+  // e % 3N), written transposed to LDS. All loads of a chunk per lane are issued before the
+  // first LDS write, so the wave waits for HBM once per chunk, not once per load. A non-finite
+  // entry flags its QP in a bit mask (one bit per QP of the wave, OR-ed over the lanes).
+  unsigned long long badq = 0ull;
   {
     const int S3 = 3 * P.xr_stride;  // floats per QP in x_ref (>= 3N)
-    const int nq = (B - b0) < 64 ? (B - b0) : 64;
     const int tot = nq * n3;
     const float* src = xrg + (size_t)b0 * S3;
     const float rn3 = 1.0f / (float)n3;
-    constexpr int kChunk = 32;
+    constexpr int kChunk = 8;
     for (int e0 = 0; e0 < tot; e0 += kChunk * 64) {
       float vbuf[kChunk];
       int dst[kChunk];
@@ -103,25 +122,33 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         q -= (q * n3 > e) ? 1 : 0;
         q += ((q + 1) * n3 <= e) ? 1 : 0;
         const int c = e - q * n3;
-        dst[j] = (e < tot) ? c * 64 + q : -1;
+        dst[j] = (e < tot) ? c * L + q : -1;
         vbuf[j] = (e < tot) ? src[(size_t)q * S3 + c] : 0.f;
       }
 #pragma unroll
-      for (int j = 0; j < kChunk; j++)
+      for (int j = 0; j < kChunk; j++) {
         if (dst[j] >= 0) xr_s[dst[j]] = vbuf[j];
+        if (!isfinite(vbuf[j])) badq |= 1ull << (dst[j] & (L - 1));  // q = dst mod L
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {  // OR over the wave (64-bit shuffles)
+      const unsigned lo = __shfl_xor((unsigned)badq, o), hi = __shfl_xor((unsigned)(badq >> 32), o);
+      badq |= ((unsigned long long)hi << 32) | lo;
     }
     __syncthreads();
   }
 
   // ---- per-lane QP data (Model::Linearize, model.cpp:30-59; fp64 of the float inputs) ----
-  const int bb = live ? b : 0;
-  const double X0 = (double)x0g[3 * bb + 0], Y0 = (double)x0g[3 * bb + 1];
-  const float fTH0 = x0g[3 * bb + 2];
+  const double X0 = (double)x0g[3 * b + 0], Y0 = (double)x0g[3 * b + 1];
+  const float fTH0 = x0g[3 * b + 2];
   const double th0 = (double)fTH0;
-  const double v = (double)ulg[2 * bb + 0], d = (double)ulg[2 * bb + 1];
+  const double v = (double)ulg[2 * b + 0], d = (double)ulg[2 * b + 1];
   const double dt = (double)P.dt;
   const double Lw = (double)0.3302f;
-  const double sn = sin(th0), cs = cos(th0), sd = sin(d), cd = cos(d);
+  double sn, cs, sd, cd;
+  sincos(th0, &sn, &cs);
+  sincos(d, &sd, &cd);
   const double sec2 = 1.0 / (cd * cd);
   const double a02 = -1 * v * sn * dt, a12 = v * cs * dt;                  // :42-43
   const double b00 = cs * dt, b10 = sn * dt;                               // :48-49
@@ -137,21 +164,21 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
   const double lb0 = (double)P.umin[0], lb1 = (double)P.umin[1];
   const double ub0 = (double)P.umax[0], ub1 = (double)P.umax[1];
 
-  // scratch slot (i, e) of this lane: sp[(8 i + e) * 64]; the PDAS state of stage i (2 bits
-  // per input: 0 free, 1 lower bound, 2 upper bound) at ap[i * 64].
-  // LDS: [3N][64] references, [N][64] PDAS state, then (SLDS) the [N][8][64] Riccati scratch
-  int* ap = reinterpret_cast<int*>(xr_s + 3 * N * 64) + lane;
+  // scratch slot (i, e) of this QP: sp[(8 i + e) * L]; the PDAS state of stage i (2 bits
+  // per input: 0 free, 1 lower bound, 2 upper bound) at ap[i * L].
+  // LDS: [3N][L] references, [N][L] PDAS state, then (SLDS) the [N][8][L] Riccati scratch
+  int* ap = reinterpret_cast<int*>(xr_s + 3 * N * L) + slot;
   ST* sp;
   if constexpr (SLDS) {
-    sp = reinterpret_cast<ST*>(xr_s + 4 * N * 64) + lane;
+    sp = reinterpret_cast<ST*>(xr_s + 4 * N * L) + slot;
   } else {
-    sp = reinterpret_cast<ST*>(scr) + (size_t)blockIdx.x * N * 8 * 64 + lane;
+    sp = reinterpret_cast<ST*>(scr) + (size_t)blockIdx.x * N * 8 * L + slot;
   }
   const int R = (2 * N + 63) / 64;  // register-row count of the wave kernel's act layout
   {
     // previous tick's active bounds seed the first pass (C5; zero masks = cold start)
     unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
-    if (ws.act && live) {
+    if (ws.act) {
       lo0 = ws.act[2 * R * b];
       hi0 = ws.act[2 * R * b + 1];
       if (R > 1) {
@@ -170,56 +197,51 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         const int ca = ((l >> (va & 63)) & 1ull) ? 1 : (((h >> (va & 63)) & 1ull) ? 2 : 0);
         st |= ca << (2 * a);
       }
-      ap[i * 64] = st;
+      ap[i * L] = st;
     }
   }
   auto ref = [&](int i, double& rx, double& ry, double& rt) {
-    rx = (double)xr_s[(3 * i + 0) * 64 + lane] - X0;
-    ry = (double)xr_s[(3 * i + 1) * 64 + lane] - Y0;
-    rt = (double)xr_s[(3 * i + 2) * 64 + lane] - th0;
+    rx = (double)xr_s[(3 * i + 0) * L + slot] - X0;
+    ry = (double)xr_s[(3 * i + 1) * L + slot] - Y0;
+    rt = (double)xr_s[(3 * i + 2) * L + slot] - th0;
   };
 
-  bool done = !live;
-  if (live) {
-    // non-finite data -> F110QP_NUMERICAL with NaN outputs (e.g. the planning stage's NaN x_ref
-    // of a scenario without a valid candidate, where the reference skips MPC::Update)
-    bool bad = !(isfinite(X0) && isfinite(Y0) && isfinite(th0) && isfinite(v) && isfinite(d));
-    for (int e = 0; e < n3; e++) bad = bad || !isfinite(xr_s[e * 64 + lane]);
-    if (bad) {
-      const float nanv = __int_as_float(0x7fc00000);
-      float* uo = uout + (size_t)b * 2 * N;
-      float* xo = xout + (size_t)b * 3 * (N + 1);
-      for (int e = 0; e < 2 * N; e++) uo[e] = nanv;
-      for (int e = 0; e < 3 * (N + 1); e++) xo[e] = nanv;
-      status_out[b] = F110QP_NUMERICAL_ID;
-      if (iters_out) iters_out[b] = 0;
-      done = true;
-    }
-  }
+  // non-finite data -> F110QP_NUMERICAL with NaN outputs (e.g. the planning stage's NaN x_ref
+  // of a scenario without a valid candidate, where the reference skips MPC::Update). Such a
+  // lane keeps sweeping (NaN) in lock step but never holds the wave back.
+  const bool bad = !(isfinite(X0) && isfinite(Y0) && isfinite(th0) && isfinite(v) && isfinite(d)) ||
+                   ((badq >> slot) & 1ull);
+  bool done = bad;
+  int iters = 0;
 #ifdef F110QP_STAMPS
   t_setup = __builtin_amdgcn_s_memtime() - t_start;
 #endif
   // Rounds: a Riccati sweep for the current active set (backward), then the forward sweep that
-  // rolls out u_i, x_i and carries the costate to re-guess the set (PDAS). No change certifies
-  // the KKT conditions and the u_i the forward sweep left in the scratch are the solution.
-  for (int pass = 0; pass < kmax; pass++) {
+  // rolls out u_i, x_i and carries the costate to re-guess the set (PDAS; after kmax passes
+  // one flip per pass, the least-index rule). No change certifies the KKT conditions and the
+  // u_i the forward sweep left in the scratch are the solution; a converged lane's further
+  // sweeps reproduce them exactly.
+  const int max_pass = P.max_iter > kmax ? P.max_iter : kmax;
+  for (int pass = 0; pass < max_pass; pass++) {
     if (__ballot(!done) == 0ull) break;
+    const bool single = pass >= kmax;
 #ifdef F110QP_STAMPS
     npass++;
 #endif
     LSTAMP(t_bw);
-    if (!done) {
+    {
       // ---- Riccati backward sweep ---------------------------------------------------------
       double rx, ry, rt;
       ref(N - 1, rx, ry, rt);  // terminal stage reuses x_ref[N-1] (mpc.cpp:228)
       double P00 = q0, P01 = 0.0, P02 = 0.0, P11 = q1, P12 = 0.0, P22 = q2;
       double p0 = -q0 * rx, p1 = -q1 * ry, p2 = -q2 * rt;
-      int nst = ap[(N - 1) * 64];
+      int nst = ap[(N - 1) * L];
       for (int i = N - 1; i >= 0; i--) {
-        ST* s = sp + (size_t)i * 8 * 64;
+        ST* s = sp + (size_t)i * 8 * L;
         const int sti = nst;
-        if (i > 0) nst = ap[(i - 1) * 64];
-        ref(i, rx, ry, rt);
+        if (i > 0) nst = ap[(i - 1) * L];
+        const double rxi = rx, ryi = ry, rti = rt;
+        if (i > 0) ref(i - 1, rx, ry, rt);  // next stage's reference, loaded a stage ahead
         // Riccati step of stage i against V_{i+1}(x) = 1/2 x'Px + p'x
         const double g0 = P00 * c0 + P01 * c1 + P02 * c2 + p0;  // P C + p
         const double g1 = P01 * c0 + P11 * c1 + P12 * c2 + p1;
@@ -241,8 +263,8 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         const double e2 = P22 + a02 * P02 + a12 * P12;
         const double Y00 = q0 + P00, Y01 = P01, Y11 = q1 + P11, Y02 = e0, Y12 = e1;
         const double Y22 = q2 + e2 + a02 * e0 + a12 * e1;
-        const double hx0 = -q0 * rx + g0, hx1 = -q1 * ry + g1;
-        const double hx2 = -q2 * rt + g2 + a02 * g0 + a12 * g1;
+        const double hx0 = -q0 * rxi + g0, hx1 = -q1 * ryi + g1;
+        const double hx2 = -q2 * rti + g2 + a02 * g0 + a12 * g1;
         // masked 2x2 solve over the free inputs of the stage (fixed ones sit on their bound)
         const int ca0 = sti & 3, ca1 = (sti >> 2) & 3;
         const bool f0 = ca0 == 0, f1 = ca1 == 0;
@@ -255,14 +277,14 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         idet = fma(idet, fma(-det, idet, 1.0), idet);
         const double I00 = f0 ? M11 * idet : 0.0, I11 = f1 ? M00 * idet : 0.0;
         const double I01 = (f0 && f1) ? -M01 * idet : 0.0;
-        const double K00 = -(I00 * X00 + I01 * X10), K01 = -(I00 * X01 + I01 * X11);
-        const double K02 = -(I00 * X02 + I01 * X12);
-        const double K10 = -(I01 * X00 + I11 * X10), K11 = -(I01 * X01 + I11 * X11);
-        const double K12 = -(I01 * X02 + I11 * X12);
+        const double K00 = -I00 * X00 - I01 * X10, K01 = -I00 * X01 - I01 * X11;
+        const double K02 = -I00 * X02 - I01 * X12;
+        const double K10 = -I01 * X00 - I11 * X10, K11 = -I01 * X01 - I11 * X11;
+        const double K12 = -I01 * X02 - I11 * X12;
         const double w0 = h0 + H00 * bA0 + H01 * bA1, w1 = h1 + H01 * bA0 + H11 * bA1;
         const double k0 = bA0 - (I00 * w0 + I01 * w1), k1 = bA1 - (I01 * w0 + I11 * w1);
-        s[0] = (ST)K00; s[64] = (ST)K01; s[128] = (ST)K02; s[192] = (ST)K10; s[256] = (ST)K11;
-        s[320] = (ST)K12; s[384] = (ST)k0; s[448] = (ST)k1;
+        s[0] = (ST)K00; s[L] = (ST)K01; s[2 * L] = (ST)K02; s[3 * L] = (ST)K10; s[4 * L] = (ST)K11;
+        s[5 * L] = (ST)K12; s[6 * L] = (ST)k0; s[7 * L] = (ST)k1;
         // V_i: P = Hxx + Hux' K, p = hx + Hux' k
         P00 = Y00 + X00 * K00 + X10 * K10;
         P01 = Y01 + X00 * K01 + X10 * K11;
@@ -277,9 +299,10 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
       LACC(acc_bw, t_bw);
       LSTAMP(t_fw);
       // ---- forward sweep: u_i = K_i x_i + k_i, x_{i+1} = A x_i + B u_i + C, costate and the
-      // PDAS re-guess. K_i, k_i come through a ring of kRing stages loaded ahead (HBM latency
-      // ~ several stages of compute); the ring index is static inside the unrolled group.
+      // PDAS re-guess. K_i, k_i come through a ring of kRing stages loaded ahead; the ring
+      // index is static inside the unrolled group.
       bool changed = false;
+      bool flipped = false;  // single-flip passes: the first violation of this sweep is taken
       {
         double x0 = 0.0, x1 = 0.0, x2 = 0.0;  // recentred x_0
         double l0 = p0, l1 = p1, l2 = p2;      // lambda_0 = P_0 x_0 + p_0 = p_0
@@ -288,35 +311,42 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         for (int t = 0; t < kRing; t++)
           if (t < N) {
 #pragma unroll
-            for (int e = 0; e < 8; e++) rg[t][e] = sp[((size_t)t * 8 + e) * 64];
+            for (int e = 0; e < 8; e++) rg[t][e] = sp[((size_t)t * 8 + e) * L];
           }
+        double rx, ry, rt;
+        ref(0, rx, ry, rt);
+        int old_n = ap[0];
         for (int i0 = 0; i0 < N; i0 += kRing) {
 #pragma unroll
           for (int t = 0; t < kRing; t++) {
             const int i = i0 + t;
             if (i < N) {
-              ST* s = sp + (size_t)i * 8 * 64;
+              ST* s = sp + (size_t)i * 8 * L;
               const double K00 = rg[t][0], K01 = rg[t][1], K02 = rg[t][2], K10 = rg[t][3];
               const double K11 = rg[t][4], K12 = rg[t][5], k0 = rg[t][6], k1 = rg[t][7];
               if (i + kRing < N) {
 #pragma unroll
-                for (int e = 0; e < 8; e++) rg[t][e] = s[(kRing * 8 + e) * 64];
+                for (int e = 0; e < 8; e++) rg[t][e] = s[(kRing * 8 + e) * L];
               }
-              const int old = ap[i * 64];
-              ref(i, rx, ry, rt);
+              const int old = old_n;
+              const double rxi = rx, ryi = ry, rti = rt;
+              if (i + 1 < N) {  // next stage's state and reference, loaded a stage ahead
+                old_n = ap[(i + 1) * L];
+                ref(i + 1, rx, ry, rt);
+              }
               const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
               const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
-              s[0] = (ST)u0; s[64] = (ST)u1;  // the solution if this sweep changes nothing
+              s[0] = (ST)u0; s[L] = (ST)u1;  // the solution if this sweep changes nothing
               // lambda_{i+1} = (I - E')(lambda_i - Q(x_i - r_i))
-              const double w0 = l0 - q0 * (x0 - rx), w1 = l1 - q1 * (x1 - ry);
-              const double w2 = l2 - q2 * (x2 - rt);
+              const double w0 = l0 - q0 * (x0 - rxi), w1 = l1 - q1 * (x1 - ryi);
+              const double w2 = l2 - q2 * (x2 - rti);
               l0 = w0; l1 = w1; l2 = w2 - a02 * w0 - a12 * w1;
               // gradient of the objective in u_i: g = R(u - ud) + B' lambda_{i+1}
               const double g0 = r0 * (u0 - ud0) + b00 * l0 + b10 * l1 + b20 * l2;
               const double g1 = r1 * (u1 - ud1) + b21 * l2;
               // PDAS re-guess (Hintermueller-Ito-Kunisch, c = 1), both inputs of the stage:
               // the multiplier of an active lower bound is g, of an active upper bound -g
-              int st = 0;
+              int st = old;
 #pragma unroll
               for (int a = 0; a < 2; a++) {
                 const int ca = (old >> (2 * a)) & 3;
@@ -324,11 +354,15 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                 const double lb = a ? lb1 : lb0, ub = a ? ub1 : ub0;
                 const bool nlo = ((ca == 1) ? g : 0.0) + (lb - u) > 0.0;
                 const bool nhi = !nlo && (((ca == 2) ? -g : 0.0) + (u - ub) > 0.0);
-                st |= (nlo ? 1 : (nhi ? 2 : 0)) << (2 * a);
+                const int nca = nlo ? 1 : (nhi ? 2 : 0);
+                if (nca != ca && !(single && flipped)) {
+                  st = (st & ~(3 << (2 * a))) | (nca << (2 * a));
+                  flipped = true;
+                }
               }
               if (st != old) {
                 changed = true;
-                ap[i * 64] = st;
+                ap[i * L] = st;
               }
               const double nx0 = x0 + a02 * x2 + b00 * u0 + c0;
               const double nx1 = x1 + a12 * x2 + b10 * u0 + c1;
@@ -339,53 +373,65 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         }
       }
       LACC(acc_fw, t_fw);
-      LSTAMP(t_out);
-      if (!changed) {
-        // KKT point: (u*, x*) from the u_i of this sweep, x* by the same fp64 rollout
-        float* uo = uout + (size_t)b * 2 * N;
-        float* xo = xout + (size_t)b * 3 * (N + 1);
-        xo[0] = x0g[3 * b + 0];  // x*_0 = x0 exactly, as the dynamics rows fix it
-        xo[1] = x0g[3 * b + 1];
-        xo[2] = fTH0;
-        double x0 = 0.0, x1 = 0.0, x2 = 0.0;
-        ST ur[kRing][2];
-#pragma unroll
-        for (int t = 0; t < kRing; t++)
-          if (t < N) { ur[t][0] = sp[(size_t)t * 8 * 64]; ur[t][1] = sp[(size_t)t * 8 * 64 + 64]; }
-        for (int i0 = 0; i0 < N; i0 += kRing) {
-#pragma unroll
-          for (int t = 0; t < kRing; t++) {
-            const int i = i0 + t;
-            if (i < N) {
-              const double u0 = (double)ur[t][0], u1 = (double)ur[t][1];
-              if (i + kRing < N) {
-                const ST* s = sp + (size_t)(i + kRing) * 8 * 64;
-                ur[t][0] = s[0];
-                ur[t][1] = s[64];
-              }
-              uo[2 * i] = (float)u0;
-              uo[2 * i + 1] = (float)u1;
-              const double nx0 = x0 + a02 * x2 + b00 * u0 + c0;
-              const double nx1 = x1 + a12 * x2 + b10 * u0 + c1;
-              const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
-              x0 = nx0; x1 = nx1; x2 = nx2;
-              xo[3 * i + 3] = (float)(x0 + X0);
-              xo[3 * i + 4] = (float)(x1 + Y0);
-              xo[3 * i + 5] = (float)(x2 + th0);
-            }
-          }
-        }
-        status_out[b] = F110QP_SOLVED_ID;
-        if (iters_out) iters_out[b] = pass;  // active-set changes before the KKT point
+      if (!changed && !done) {  // KKT point: the u_i of this sweep (in the scratch) are u*
         done = true;
+        iters = pass + 1;  // equality-QP solves incl. the confirming one
       }
-      LACC(acc_out, t_out);
     }
   }
-  if (live && ws.act && done) {  // active set of this solution for the next tick
+  // ---- output sweep, every lane at once: x* by the fp64 rollout of u* ----
+  LSTAMP(t_out);
+  {
+    const bool solved = done && !bad;
+    const float nanv = __int_as_float(0x7fc00000);
+    float* uo = uout + (size_t)b * 2 * N;
+    float* xo = xout + (size_t)b * 3 * (N + 1);
+    if (owner) {
+      xo[0] = solved ? x0g[3 * b + 0] : nanv;  // x*_0 = x0 exactly, as the dynamics rows fix it
+      xo[1] = solved ? x0g[3 * b + 1] : nanv;
+      xo[2] = solved ? fTH0 : nanv;
+    }
+    double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+    ST ur[kRing][2];
+#pragma unroll
+    for (int t = 0; t < kRing; t++)
+      if (t < N) { ur[t][0] = sp[(size_t)t * 8 * L]; ur[t][1] = sp[(size_t)t * 8 * L + L]; }
+    for (int i0 = 0; i0 < N; i0 += kRing) {
+#pragma unroll
+      for (int t = 0; t < kRing; t++) {
+        const int i = i0 + t;
+        if (i < N) {
+          const double u0 = (double)ur[t][0], u1 = (double)ur[t][1];
+          if (i + kRing < N) {
+            const ST* s = sp + (size_t)(i + kRing) * 8 * L;
+            ur[t][0] = s[0];
+            ur[t][1] = s[L];
+          }
+          const double nx0 = x0 + a02 * x2 + b00 * u0 + c0;
+          const double nx1 = x1 + a12 * x2 + b10 * u0 + c1;
+          const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
+          x0 = nx0; x1 = nx1; x2 = nx2;
+          if (owner) {
+            uo[2 * i] = solved ? (float)u0 : nanv;
+            uo[2 * i + 1] = solved ? (float)u1 : nanv;
+            xo[3 * i + 3] = solved ? (float)(x0 + X0) : nanv;
+            xo[3 * i + 4] = solved ? (float)(x1 + Y0) : nanv;
+            xo[3 * i + 5] = solved ? (float)(x2 + th0) : nanv;
+          }
+        }
+      }
+    }
+    if (owner) {
+      // OSQP status ids: solved; no KKT point within max_pass passes -> max-iter
+      status_out[b] = bad ? F110QP_NUMERICAL_ID : (done ? F110QP_SOLVED_ID : F110QP_MAX_ITER_ID);
+      if (iters_out) iters_out[b] = bad ? 0 : (done ? iters : max_pass);
+    }
+  }
+  LACC(acc_out, t_out);
+  if (owner && ws.act) {  // active set of this solution for the next tick
     unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
     for (int i = 0; i < N; i++) {
-      const int st = ap[i * 64];
+      const int st = ap[i * L];
 #pragma unroll
       for (int a = 0; a < 2; a++) {
         const int va = 2 * i + a, ca = (st >> (2 * a)) & 3;
@@ -404,62 +450,70 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
       ws.act[2 * (R * b + 1) + 1] = hi1;
     }
   }
-  if (live && !done) fail_list[atomicAdd(fail_count, 1)] = b;  // -> wave kernel (GI)
 #ifdef F110QP_STAMPS
   if (lane == 0 && blockIdx.x < 4096) {
     unsigned long long* o = g_lstamps + (size_t)blockIdx.x * kLaneStampSlots;
-    o[0] = t_setup; o[1] = acc_bw; o[2] = acc_fw; o[3] = acc_adj; o[4] = acc_out;
+    o[0] = t_setup; o[1] = acc_bw; o[2] = acc_fw; o[3] = 0; o[4] = acc_out;
     o[5] = npass; o[6] = __builtin_amdgcn_s_memtime() - t_start; o[7] = 0;
   }
 #endif
 }
 
 template <typename ST, bool SLDS>
-static hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul,
+static hipError_t launch_lane_t(const KParams& P, int B, int L, const float* x0, const float* ul,
                                 const float* xr, float* uo, float* xo, int* st, int* its,
                                 const WarmState& ws, const LaneWork& lw, size_t lds,
                                 hipStream_t s) {
-  const int waves = (B + 63) / 64;
+  const int waves = (B + L - 1) / L;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_kernel<ST, SLDS>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((lane_kernel<ST, SLDS>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr,
-                     uo, xo, st, its, lw.scratch, lw.fail_list, lw.fail_count,
-                     lw.fail_count_next, ws, lw.kmax);
+  hipLaunchKernelGGL((lane_kernel<ST, SLDS>), dim3(waves), dim3(64), lds, s, P, B, L, x0, ul, xr,
+                     uo, xo, st, its, lw.scratch, ws, lw.kmax);
   return hipGetLastError();
 }
 
-// LDS per wave: the staged references (12 N * 64 B) + Riccati scratch (8 N * 64 * sizeof(ST))
-// + PDAS state (4 N * 64 B) (lane_mode 0 = auto; 1/2/3/4 force LDS fp64 / LDS fp32 / HBM fp64 /
-// HBM fp32).
+// QPs per wave: the smallest power of two (<= 64) that fits the batch in kLaneTargetWaves waves
+// (one per CU).
+int lane_qps_per_wave(int B, int qpw) {
+  if (qpw >= 1 && qpw <= 64 && (qpw & (qpw - 1)) == 0) return qpw;
+  int L = 1;
+  while (L < 64 && (B + L - 1) / L > kLaneTargetWaves) L <<= 1;
+  return L;
+}
+
+// LDS per wave: the staged references (12 N L B) + PDAS state (4 N L B) + Riccati scratch
+// (8 N L sizeof(ST)) (lane_mode 0 = auto; 1/2/3/4 force LDS fp64 / LDS fp32 / HBM fp64 / HBM
+// fp32).
 hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* ul,
                        const float* xr, float* uo, float* xo, int* st, int* its,
                        const WarmState& ws, const LaneWork& lw, hipStream_t s) {
   if (B <= 0) return hipSuccess;
+  const int L = lane_qps_per_wave(B, lw.qpw);
   const size_t N = (size_t)P.N;
-  const size_t base = N * 64 * (12 + 4);  // references + PDAS state
-  const size_t lds64 = base + N * 8 * 64 * sizeof(double), lds32 = base + N * 8 * 64 * sizeof(float);
+  const size_t base = N * L * (12 + 4);  // references + PDAS state
+  const size_t lds64 = base + N * 8 * L * sizeof(double), lds32 = base + N * 8 * L * sizeof(float);
   const size_t cap = 160 * 1024;
   int mode = lw.mode;
-  // auto: fp64 scratch in LDS while one wave per CU covers the batch (latency), else fp32
-  // scratch in the HBM workspace: it halves the scratch traffic that binds large batches, and
-  // with the state recentred on x0 the fp32 gains and trajectories stay within ~1e-7 of the
-  // exact optimum (tests/test_gpu_parity.py::test_lane_backend_scratch_modes). Where fp64 does
-  // not fit one wave per CU (N > 24) the fp32 scratch still does: LDS fp32 beats HBM fp32 there
-  // (C4 shard 8,192 x N = 40: 236.5 vs 261.0 us).
+  // auto: the scratch in LDS when every wave of the grid is resident with it (waves per CU x
+  // its LDS within the CU's 160 KiB): fp64 if that fits, else fp32; otherwise fp32 in the HBM
+  // workspace (the waves then stay resident on the 16 N L bytes of references + state alone).
+  // With the state recentred on x0 the fp32 gains and trajectories stay within ~1e-7 of the
+  // exact optimum (tests/test_gpu_parity.py::test_lane_backend_scratch_modes).
   if (mode == 0) {
-    const bool one_wave_per_cu = (B + 63) / 64 <= 256;
-    mode = one_wave_per_cu && lds64 <= cap ? 1 : one_wave_per_cu && lds32 <= cap ? 2 : 4;
+    const size_t waves = ((size_t)B + L - 1) / L;
+    const size_t per_cu = (waves + 255) / 256;
+    mode = per_cu * lds64 <= cap ? 1 : per_cu * lds32 <= cap ? 2 : 4;
   }
   if (mode == 1 && lds64 <= cap)
-    return launch_lane_t<double, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds64, s);
+    return launch_lane_t<double, true>(P, B, L, x0, ul, xr, uo, xo, st, its, ws, lw, lds64, s);
   if (mode == 2 && lds32 <= cap)
-    return launch_lane_t<float, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds32, s);
-  if (mode == 4)
-    return launch_lane_t<float, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
-  return launch_lane_t<double, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
+    return launch_lane_t<float, true>(P, B, L, x0, ul, xr, uo, xo, st, its, ws, lw, lds32, s);
+  if (mode == 4 || mode == 2)
+    return launch_lane_t<float, false>(P, B, L, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
+  return launch_lane_t<double, false>(P, B, L, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
 }
 
 }  // namespace f110qp

@@ -395,20 +395,38 @@ def test_lane_backend_custom_weights_and_far_origin(oracle, capi, be):
 
 
 @pytest.mark.parametrize("be", RICCATI)
-def test_lane_backend_hands_over_to_wave_kernel(oracle, capi, monkeypatch, be):
-    """F110QP_LANE_KMAX=1 lets no QP with an active bound settle in the lane kernel: those go
-    through the device-side list to the wave kernel (GI). Results stay exact, and a second call
-    on the same context reuses the other list counter."""
-    monkeypatch.setenv("F110QP_LANE_KMAX", "1")
-    N = 20
-    w = workload.make_batch(3000, N, seed=991, heading="true", lateral=1.5, steer_range=1.0)
+@pytest.mark.parametrize("kmax,N", [("0", 20), ("1", 20), ("2", 40), ("0", 40)])
+def test_lane_backend_single_flip_fallback(oracle, capi, monkeypatch, be, kmax, N):
+    """F110QP_LANE_KMAX caps the multi-flip PDAS passes of the lane kernel; past the cap a QP
+    flips one complementarity violation per pass (least index, stage-major), so the QPs with
+    many active bounds finish inside the same launch in more passes. kmax = 0: single flips
+    from the first pass. Results stay exact, repeated calls on one context agree, and the pass
+    counts exceed the PDAS ones."""
+    monkeypatch.setenv("F110QP_LANE_KMAX", kmax)
+    w = workload.make_batch(3000, N, seed=991 + N, heading="true", lateral=1.5, steer_range=1.0)
     s = capi.Solver(capi.default_config(N, backend=_be(capi, be)))
     ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"])
-    for _ in range(3):
+    for _ in range(2):
         u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
         np.testing.assert_array_equal(st, sr)
         assert rel_err(u, ur).max() <= TOL and rel_err(x, xr).max() <= TOL
     s.close()
+    monkeypatch.delenv("F110QP_LANE_KMAX")
+    s = capi.Solver(capi.default_config(N, backend=_be(capi, be)))
+    _, _, _, it_pdas = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    assert it.max() > it_pdas.max()
+
+
+@pytest.mark.parametrize("qpw", ["1", "2", "8", "64"])
+def test_lane_backend_qps_per_wave(oracle, capi, monkeypatch, qpw):
+    """Every QPs-per-wave layout of the lane kernel (F110QP_LANE_QPW; auto picks by batch)
+    gives the same exact results; the batch is not a multiple of the wave width."""
+    monkeypatch.setenv("F110QP_LANE_QPW", qpw)
+    N, B = 40, 700
+    w = workload.make_batch(B, N, seed=5150, heading="true", lateral=1.2, steer_range=0.8)
+    u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE, tol=2e-6)
+    assert (st == capi.SOLVED).all()
 
 
 @pytest.mark.parametrize("cap", ["0", "1", "2"])
