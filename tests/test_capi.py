@@ -30,7 +30,7 @@ def test_library_is_gfx950_code_object(capi):
 
 def test_version_and_defaults(capi):
     L = capi.load()
-    assert L.f110qp_version() == 3
+    assert L.f110qp_version() == 4
     c = capi.default_config(20)
     # params.yaml:1-13,42-47 and constraints.cpp:19,21
     assert c.horizon == 20 and c.dt == np.float32(0.01)
