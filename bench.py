@@ -79,25 +79,49 @@ def flops_per_qp(N: int, passes: float, pivots: float, gap: bool = False) -> flo
     return base + passes * 2 * n * n + pivots * 2 * n * n
 
 
-def load_traffic(config: str, kernel: str):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary of this config, if it was
-    taken on the same kernel (tools/profile_round.sh + tools/summarize_profiles.py)."""
+def load_traffic(config: str, batch: int, horizon: int, backend: str):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary of this config
+    (tools/profile_round.sh + tools/summarize_profiles.py), only when it was taken on the same
+    (config, batch, horizon, back end); None otherwise."""
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch") if kernel in d.get("kernel", "") else None
     except Exception:
         return None
+    key = (d.get("config"), d.get("batch"), d.get("horizon"), d.get("backend"))
+    return d.get("hbm_bytes_per_launch") if key == (config, batch, horizon, backend) else None
 
 
-def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int):
+def cpu_threads_default() -> int:
+    """Host threads for the throughput baseline: the CPUs this process may run on, capped by
+    OMP_NUM_THREADS when the environment sets it (the GPU box sets it to its per-GPU CPU share;
+    nproc there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(omp)) if omp.isdigit() and int(omp) > 0 else n
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int, c1_ticks: int):
     """Time the reference's algorithm on the host cores: oracle/osqp_admm.c, a restatement of
     OSQP 0.6 with the settings MPC::Update uses (defaults + warm start; mpc.cpp:98-133) on the
     reference's own sparse QP (re-scaled and re-factored per tick, as OSQP must when A changes).
-    The independent QPs of a batch start cold. Also reports the exact fp64 oracle's rate."""
+    The independent QPs of a batch start cold. Also reports the exact fp64 oracle's rate, and
+    BASELINE configs[0] (C1): single horizon-20 QP ticks on ONE core (MPC::Update solves one QP
+    per odometry tick, mpc.cpp:133 / project.cpp:188), p50/p99 over c1_ticks ticks, both solvers."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker only: used here for the cpu_baseline leg, never for the GPU value
     from f110qp import workload
@@ -129,7 +153,24 @@ def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int):
         el2 = time.perf_counter() - t1
         if el2 >= max(2.0, seconds / 5):
             break
+    # C1: one core, one QP per tick, horizon 20 (configs[0]), timed per tick inside C
+    c1 = {}
+    if c1_ticks > 0:
+        w1 = workload.make_batch(1024, 20, seed=777)
+        prm1 = oracle.params(20)
+        for name, exact in (("osqp_admm_restatement", False), ("exact_oracle", True)):
+            ns, nsol = oracle.tick_latency(prm1, st, w1["x0"], w1["u_lin"], w1["x_ref"], c1_ticks, exact=exact)
+            us = ns / 1e3
+            c1[name] = {"p50_us": float(np.percentile(us, 50)), "p99_us": float(np.percentile(us, 99)),
+                        "mean_us": float(us.mean()), "ticks": int(c1_ticks), "solved": nsol,
+                        "qps_one_core": float(1e6 / us.mean())}
+        c1["note"] = ("C1 = BASELINE configs[0]: single horizon-20 QP per tick on one core (calling thread), "
+                      "wall time of the whole solve per tick; instances cycle over 1,024 seeded ticks")
     return dict(value=n / el, unit="QP solves/s", cores=threads, kind="port",
+                host={"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+                      "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "cpu_model": cpu_model(),
+                      "threads_used": threads},
+                c1_single_core=c1,
                 sample=f"{n} QPs ({n // B} x {B} {config} ticks, horizon {N}) in {el:.1f} s: oracle/osqp_admm.c "
                        f"(OSQP 0.6 defaults restated: Ruiz scaling, rho=0.1 adaptive, sigma=1e-6, alpha=1.6, "
                        f"eps=1e-3, check every 25, banded LDL' KKT) with OpenMP over QPs; mean ADMM iters "
@@ -202,7 +243,10 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="override batch per GPU")
     ap.add_argument("--horizon", type=int, default=0, help="override the config's horizon N")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the throughput baseline (0: the affinity CPU count, capped by "
+                         "OMP_NUM_THREADS when set)")
+    ap.add_argument("--c1-ticks", type=int, default=10000, help="single-core C1 ticks per solver (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse several "
@@ -401,7 +445,7 @@ def main():
         cpeak, cname = FP32_PEAK_TFLOPS, "fp32_compute"
     achieved_gbs = bpq * Bper / (kms * 1e-3) / 1e9
     achieved_tf = fpq * Bper / (kms * 1e-3) / 1e12
-    traffic = load_traffic(args.config, "lane_kernel" if be_name == "lane" else "solve_kernel")
+    traffic = load_traffic(args.config, Bper, N, be_name)
 
     out = {
         "metric": f"QP solves/s (horizon={N}, nx=3 reference model, nu=2)",
@@ -441,7 +485,7 @@ def main():
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
             "kernel": {"wave": "f110qp::solve_kernel",
-                       "lane": "f110qp::lane_kernel (+ solve_kernel hand-over launch)"}[be_name],
+                       "lane": "f110qp::lane_kernel (the only launch of the step)"}[be_name],
             "kernel_ms_per_launch": kms,
             "algorithmic_bytes_per_qp": bpq,
             cname: {"achieved": achieved_tf, "peak": cpeak, "unit": "TFLOP/s",
@@ -456,7 +500,8 @@ def main():
         out["latency"] = latency
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.config, N, gap, args.cpu_seconds, args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(args.config, N, gap, args.cpu_seconds,
+                                               args.cpu_threads or cpu_threads_default(), args.c1_ticks)
         except Exception as e:  # the baseline must never take the GPU number down
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

@@ -30,8 +30,8 @@ BACKEND_WAVE = 1
 BACKEND_LANE = 2
 LANE_MIN_BATCH = 4096
 LANE_MIN_BATCH_WIDE = 1025
-LANE_MIN_BATCH_GROUPED = 16384
-LANE_MIN_BATCH_GROUPED_WIDE = 16384
+LANE_MIN_BATCH_GROUPED = LANE_MIN_BATCH
+LANE_MIN_BATCH_GROUPED_WIDE = LANE_MIN_BATCH_WIDE
 
 
 def auto_backend(horizon: int, batch: int, gap: bool, grouped: bool = False) -> int:

@@ -31,8 +31,13 @@
  *      halfspace [B][2][3]   (l1, l2) = (a, b, c+0.5) from FindHalfSpaces, or NULL
  *      u_out     [B][N][2]   u*_k = z[3(N+1)+2k .. +1]            (mpc.cpp:148-157)
  *      x_out     [B][N+1][3] x*_k = z[3k .. 3k+2]                 (mpc.cpp:167-169)
- *      status    [B]         F110QP_SOLVED / _PRIMAL_INFEASIBLE / _MAX_ITER (OSQP codes)
- *      iters     [B]         active-set iterations (may be NULL)
+ *      status    [B]         F110QP_SOLVED / _PRIMAL_INFEASIBLE / _MAX_ITER / _NUMERICAL
+ *                            (OSQP codes)
+ *      iters     [B]         active-set iterations (may be NULL): box-only QPs on either back end
+ *                            count the equality-QP solves of the primal-dual active set including
+ *                            the final one that confirms the KKT point (0 would mean none ran);
+ *                            QPs the wave back end hands to its Goldfarb-Idnani loop (gap rows,
+ *                            or a box PDAS that did not settle) count GI iterations instead
  *    On a non-SOLVED status u_out/x_out hold NaN, as OSQP's solution does on failure.
  */
 #ifndef F110QP_H
@@ -61,17 +66,21 @@ extern "C" {
 #define F110QP_GAP_ACTIVE 1       /* a*x+b*y >= -(c+0.5) on stages 1..N (mpc.cpp:297-298) */
 
 /* solver back ends (f110qp_config.backend) */
-#define F110QP_BACKEND_AUTO 0     /* lane-per-QP for box-only batches >= F110QP_LANE_MIN_BATCH */
-                                  /* (N <= 32) or >= F110QP_LANE_MIN_BATCH_WIDE (N > 32)      */
-#define F110QP_BACKEND_WAVE 1     /* one wavefront per QP: condensed W = H^-1 + PDAS/GI        */
-#define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64 (box rows only;     */
-                                  /* gap rows always use the wave back end)                   */
-#define F110QP_LANE_MIN_BATCH 4096       /* measured wave/lane crossover on MI355X, N = 20 */
-#define F110QP_LANE_MIN_BATCH_WIDE 1025  /* N > 32: beyond one wave per SIMD (1,024 QPs)   */
-/* grouped calls (f110qp_solve_grouped*): the wave back end reuses one W = H^-1 per group, so it
- * stays ahead of the lane back end up to these batch sizes (measured) */
-#define F110QP_LANE_MIN_BATCH_GROUPED 16384
-#define F110QP_LANE_MIN_BATCH_GROUPED_WIDE 16384
+#define F110QP_BACKEND_AUTO 0     /* lane-per-QP for box-only batches >= F110QP_LANE_MIN_BATCH  */
+                                  /* (N <= 32) or >= F110QP_LANE_MIN_BATCH_WIDE (N > 32)       */
+#define F110QP_BACKEND_WAVE 1     /* one wavefront per QP: condensed W = H^-1 + PDAS/GI         */
+#define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64 (box rows only;      */
+                                  /* gap rows always use the wave back end)                    */
+/* AUTO thresholds, measured on MI355X (kernel us). N = 20: wave 78 vs lane 88
+ * at 4,096 cold QPs of the C2 recipe, but lane 80 vs wave 100 on the C5 stream's cold tick and
+ * 39 vs 91 warm; 141 vs 91 at 8,192. N = 30: crossover near 3,800. N = 40: wave 105 vs lane 200
+ * at 512, 194 vs 201 at 1,024, lane beyond. Grouped calls use the same thresholds: the wave back
+ * end's per-group W saves its inverse but its per-QP active-set phase still dominates (C4
+ * candidate sets: 8,192 x N=40 grouped wave 1,041 us vs lane 240 us). */
+#define F110QP_LANE_MIN_BATCH 4096
+#define F110QP_LANE_MIN_BATCH_WIDE 1025
+#define F110QP_LANE_MIN_BATCH_GROUPED F110QP_LANE_MIN_BATCH
+#define F110QP_LANE_MIN_BATCH_GROUPED_WIDE F110QP_LANE_MIN_BATCH_WIDE
 
 #define F110QP_MAX_HORIZON 48  /* 2N <= 96 decision variables: two register rows per lane */
 
@@ -134,9 +143,9 @@ int f110qp_solve_batch_dev(f110qp_ctx* ctx, int batch, const float* x0, const fl
  * One W per group is built from its first member; every member whose (x0[b][2], u_lin[b]) bits
  * equal that member's reuses it, any other QP (or an id outside [0, num_groups)) builds its own.
  * Grouping therefore never changes a result: the output is bit-identical to
- * f110qp_solve_batch[_dev] on the wave back end. The lane back end (chosen by AUTO above
- * F110QP_LANE_MIN_BATCH_GROUPED[_WIDE]) factors per QP and ignores the groups. Grouped calls
- * neither use nor update the warm-start state. Same layouts and conventions as above. */
+ * f110qp_solve_batch[_dev] on the wave back end. The lane back end (chosen by AUTO at and above
+ * F110QP_LANE_MIN_BATCH_GROUPED[_WIDE]) has no factor to share and ignores the groups. Grouped
+ * calls neither use nor update the warm-start state. Same layouts and conventions as above. */
 int f110qp_solve_grouped(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
                          const float* x_ref, const float* halfspace, const int* group,
                          int num_groups, float* u_out, float* x_out, int* status, int* iters);

@@ -114,6 +114,10 @@ int f110o_admm_solve_batch(const f110o_params* prm, const f110o_admm_settings* s
                            const float* x0, const float* u_lin, const float* x_ref,
                            const float* hs, int gap_active, double* u_out, int* status,
                            int* iters, int num_threads);
+/* single-QP ticks on the calling thread (C1 baseline): ns_out[t] per tick; exact = 1 -> f110o_solve */
+int f110o_tick_latency(const f110o_params* prm, const f110o_admm_settings* s, int exact, int batch,
+                       const float* x0, const float* u_lin, const float* x_ref, const float* hs,
+                       int gap_active, int ticks, double* ns_out);
 
 /* ---- planning stage in front of MPC::Update (plan_oracle.c; project.cpp:64-152) ---------- */
 typedef struct {

@@ -108,6 +108,8 @@ def lib():
                                            dp, C.c_int, dp, dp, ip]
             L.f110o_admm_solve_batch.argtypes = [C.POINTER(Params), C.POINTER(AdmmSettings), C.c_int,
                                                  fp, fp, fp, fp, C.c_int, dp, ip, ip, C.c_int]
+            L.f110o_tick_latency.argtypes = [C.POINTER(Params), C.POINTER(AdmmSettings), C.c_int, C.c_int,
+                                             fp, fp, fp, fp, C.c_int, C.c_int, dp]
         pp = C.POINTER(PlanParams)
         up = C.POINTER(C.c_ubyte)
         L.f110o_default_plan_params.argtypes = [pp]
@@ -271,6 +273,23 @@ def admm_solve_batch(prm: Params, settings: AdmmSettings, x0, u_lin, x_ref, hs=N
                                  _ptr(h, fp), int(gap_active), _ptr(u), _ptr(st, C.c_int), _ptr(it, C.c_int),
                                  int(num_threads))
     return u, st, it
+
+
+def tick_latency(prm: Params, settings: AdmmSettings, x0, u_lin, x_ref, ticks: int, exact: bool = False,
+                 hs=None, gap_active=False):
+    """C1 baseline: `ticks` single-QP solves on the calling thread (one core), instance t % B each;
+    returns the wall nanoseconds of every tick (timed inside C) and the number solved."""
+    N = prm.horizon
+    x0 = np.ascontiguousarray(x0, np.float32)
+    B = x0.shape[0]
+    ul = np.ascontiguousarray(u_lin, np.float32)
+    xr = np.ascontiguousarray(x_ref, np.float32)
+    h = None if hs is None else np.ascontiguousarray(hs, np.float32).reshape(B, 6)
+    ns = np.zeros(ticks)
+    fp = C.c_float
+    nsol = lib().f110o_tick_latency(C.byref(prm), C.byref(settings), int(exact), B, _ptr(x0, fp), _ptr(ul, fp),
+                                    _ptr(xr, fp), _ptr(h, fp), int(gap_active), int(ticks), _ptr(ns))
+    return ns, int(nsol)
 
 
 # ---- planning stage (plan_oracle.c) ------------------------------------------------------------

@@ -19,7 +19,9 @@
  *     QDLDL with an AMD ordering is replaced by a banded LDL' in a stage-interleaved ordering
  *     of the MPC KKT (bandwidth 17 at any horizon): the same O(n) factor cost class.
  */
+#define _POSIX_C_SOURCE 199309L
 #include <math.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -381,5 +383,44 @@ int f110o_admm_solve_batch(const f110o_params* prm, const f110o_admm_settings* s
     free(xr);
     free(z);
   }
+  return nsolved;
+}
+
+/* C1 CPU baseline (BASELINE configs[0]): single-QP control ticks on the CALLING
+ * thread, one core, as MPC::Update solves one QP per odometry tick (src/mpc.cpp:133,
+ * src/project.cpp:188). Tick t solves instance t % batch; ns_out[t] = wall nanoseconds of that
+ * tick's whole solve (set-up + factorisation + iterations + solution), clock_gettime MONOTONIC.
+ * exact = 0: the OSQP-0.6-defaults ADMM restatement (cold per tick, as the batch baseline);
+ * exact = 1: the exact condensed active-set oracle. Returns the number of SOLVED ticks. */
+int f110o_tick_latency(const f110o_params* prm, const f110o_admm_settings* s, int exact, int batch,
+                       const float* x0, const float* u_lin, const float* x_ref, const float* hs,
+                       int gap_active, int ticks, double* ns_out) {
+  const int N = prm->horizon, n = f110o_num_variables(N);
+  double* xr = (double*)malloc(3 * N * sizeof(double));
+  double* z = (double*)malloc(n * sizeof(double));
+  double* u = (double*)malloc(2 * N * sizeof(double));
+  double* x = (double*)malloc(3 * (N + 1) * sizeof(double));
+  int nsolved = 0;
+  f110o_admm_settings cold = *s;
+  cold.warm_start = 0;
+  for (int t = 0; t < ticks; t++) {
+    const int b = t % batch;
+    double xx[3], uu[2], hh[6];
+    for (int k = 0; k < 3; k++) xx[k] = x0[3 * b + k];
+    for (int k = 0; k < 2; k++) uu[k] = u_lin[2 * b + k];
+    for (int k = 0; k < 3 * N; k++) xr[k] = x_ref[(size_t)b * 3 * N + k];
+    if (hs) for (int k = 0; k < 6; k++) hh[k] = hs[6 * b + k];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    int st, it = 0;
+    if (exact)
+      st = f110o_solve(prm, xx, uu, xr, hs ? hh : NULL, gap_active, u, x, NULL, NULL, NULL, NULL);
+    else
+      st = f110o_admm_solve(prm, &cold, xx, uu, xr, hs ? hh : NULL, gap_active, z, NULL, &it);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    ns_out[t] = (double)(t1.tv_sec - t0.tv_sec) * 1e9 + (double)(t1.tv_nsec - t0.tv_nsec);
+    nsolved += st == F110O_SOLVED;
+  }
+  free(xr); free(z); free(u); free(x);
   return nsolved;
 }

@@ -61,6 +61,10 @@ def main():
         B = bench["config"]["batch_per_gpu"]
         hbm = (fetch + write) * 1024 if fetch is not None and write is not None else None
         out = {
+            "config": c.split("@")[0],
+            "batch": B,
+            "horizon": bench["config"]["horizon"],
+            "backend": be,
             "kernel": f"f110qp::{kname} (config {c}: {B} QPs, N={bench['config']['horizon']}, {bench['config']['backend']})",
             "passes": f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of bench.py --no-cpu --config {c} --steps 20",
             "rocprof_avg_kernel_us": avg_us,
@@ -71,7 +75,7 @@ def main():
             "hbm_bytes_per_launch": hbm,
             "hbm_bytes_per_qp": hbm / B if hbm else None,
             "algorithmic_bytes_per_qp": bench["roofline"]["algorithmic_bytes_per_qp"],
-            "note": "FETCH_SIZE/WRITE_SIZE are KB (x1024), summed over the kernel's dispatches and averaged; raw (no gfx950 2x correction: the kernels' reads are narrow gathers, not wide coalesced streams).",
+            "note": "FETCH_SIZE/WRITE_SIZE are KB (x1024), summed over the kernel's dispatches and averaged; raw. MI355X_MICROARCH.md: gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane streaming reads and other widths are uncalibrated; these kernels read with 4-B (x_ref staging) and 4/8-B (scratch) lanes, so the read share may be under-reported by up to 2x.",
         }
         json.dump(out, open(os.path.join(ROOT, "profiles", f"pmc_{c}.json"), "w"), indent=1)
         print(c, json.dumps(out))
