@@ -28,10 +28,14 @@ sys.path.insert(0, os.path.join(ROOT, "f110-mpc_amd"))
 CONFIGS = {
     # name: (batch per GPU, horizon, gap rows active, warm-started stream, description)
     "c2": (1024, 20, False, False, "configs[1]: batch=1024 QPs, horizon=20, box constraints only"),
-    "c3": (4096, 20, True, False, "configs[2]: batch=4096 QPs, horizon=20, + half-space gap constraints"),
-    "c5": (4096, 20, False, True, "configs[4]: batch=4096 QPs, horizon=20, warm-started receding-horizon "
-                                   "stream (x0 advances 4.5*dt per step, KKT factor reused)"),
-    "c5_cold": (4096, 20, False, False, "configs[4] stream solved cold (no warm start), for comparison"),
+    "c3": (4096, 20, True, False, "configs[2]: batch=4096 QPs, horizon=20, + half-space gap constraints "
+                                  "(FindHalfSpaces of one 1,080-beam scan per QP inside every step)"),
+    "c5": (4096, 20, False, True, "configs[4]: batch=4096 QPs, horizon=20, warm-started closed receding-horizon "
+                                   "loop (x0 <- simulate_dynamics(x0, u*_0), u_lin = (4.5, steer of u*_1), "
+                                   "mini path re-planned every 5 ticks; previous tick's active set seeds the solve)"),
+    "c5_cold": (4096, 20, False, False, "configs[4] closed-loop stream solved cold (no warm start), for comparison"),
+    "c5_straight": (4096, 20, False, True, "best case, not configs[4]: warm stream whose x0 slides along a fixed "
+                                           "heading with fixed u_lin and x_ref (every linearisation key repeats)"),
     "c2_big": (65536, 20, False, False, "throughput: batch=65536 QPs, horizon=20, box constraints"),
     # global batch, sharded over the ranks (strong scaling): 546 scenarios x 120 candidates + 16
     "c4": (65536, 40, False, False, "configs[3]: batch=65536 QPs, horizon=40, 6-lane x 20 mini-trajectory "
@@ -319,7 +323,19 @@ def main():
     elif stream_cfg:
         # one tick of the stream per step, all ticks staged in HBM before timing
         nt = args.warmup + args.steps + 20
-        ticks = workload.make_stream(Bper, N, nt, seed=1000 + rank)
+        if args.config == "c5_straight":
+            ticks = workload.make_stream(Bper, N, nt, seed=1000 + rank)
+        else:
+            # the closed loop is generated once, before timing, by a cold solver of the same back end
+            # (its u*_0 drives the simulated car); the timed steps replay the recorded ticks
+            gen_cfg = capi.default_config(N, device=dev.index, backend={"auto": capi.BACKEND_AUTO, "wave":
+                                          capi.BACKEND_WAVE, "lane": capi.BACKEND_LANE}[args.backend])
+            gen = capi.Solver(gen_cfg)
+            ticks = workload.closed_loop_stream(lambda a, b_, c: gen.solve(a, b_, c)[0], Bper, N, nt,
+                                                seed=1000 + rank)
+            gen.close()
+        key_hit = workload.warm_key_hit_rate(ticks)
+        IT = torch.empty((nt, Bper), dtype=torch.int32, device=dev)
         X0 = torch.from_numpy(np.stack([t["x0"] for t in ticks])).to(dev)
         UL = torch.from_numpy(np.stack([t["u_lin"] for t in ticks])).to(dev)
         XR = torch.from_numpy(np.stack([t["x_ref"] for t in ticks])).to(dev)
@@ -331,9 +347,11 @@ def main():
     xr = torch.from_numpy(w["x_ref"]).to(dev)
     hs = None
     if gap:
+        # one 1,080-beam LaserScan per QP, resident in HBM; FindHalfSpaces runs inside every step
+        # (MPC::Update calls it per tick, mpc.cpp:75)
         ranges, amin, ainc, amax = workload.make_scans(Bper, seed=2000 + rank)
+        rng_d = torch.from_numpy(ranges).to(dev)
         hs = torch.empty((Bper, 2, 3), dtype=torch.float32, device=dev)
-        capi.find_half_spaces_dev(x0, torch.from_numpy(ranges).to(dev), amin, ainc, amax, hs)
     uo = torch.empty((Bper, N, 2), dtype=torch.float32, device=dev)
     xo = torch.empty((Bper, N + 1, 3), dtype=torch.float32, device=dev)
     st = torch.empty((Bper,), dtype=torch.int32, device=dev)
@@ -358,7 +376,12 @@ def main():
         capi.plan_batch_dev(pcfg, ppose, pranges, sc["angle_min"], sc["angle_inc"], sc["angle_max"], ptab, pwp,
                             pxr, px0, pbt, pbg, pst, stream=stream)
 
+    def hs_step():
+        capi.find_half_spaces_dev(x0, rng_d, amin, ainc, amax, hs, stream=stream)
+
     def step():
+        if gap:
+            hs_step()
         if tick_cfg:
             plan_step()
             # scenarios without a valid candidate keep NaN x_ref and come back non-solved,
@@ -367,7 +390,7 @@ def main():
         elif stream_cfg:
             t = tick[0] % X0.shape[0]  # the latency probe after the timed region wraps around
             tick[0] += 1
-            solver.solve_dev(X0[t], UL[t], XR[t], hs, uo, xo, st, it, stream=stream)
+            solver.solve_dev(X0[t], UL[t], XR[t], hs, uo, xo, st, IT[t], stream=stream)
         elif grouped:
             solver.solve_grouped_dev(x0, ul, xr, hs, gid, ngroups, uo, xo, st, it, stream=stream)
         else:
@@ -389,9 +412,9 @@ def main():
     if world > 1:
         el = allreduce(el, dist.ReduceOp.MAX)
 
-    # solver statistics of the last step (all steps solve the same batch)
+    # solver statistics of the last step (all steps solve the same batch); streams: every timed tick
     stn = st.cpu().numpy()
-    itn = it.cpu().numpy()
+    itn = IT[args.warmup:args.warmup + args.steps].cpu().numpy() if stream_cfg else it.cpu().numpy()
     solved = float((stn == capi.SOLVED).mean())
 
     # dominant kernel duration: HIP events on the launch stream around back-to-back launches
@@ -407,6 +430,15 @@ def main():
     torch.cuda.synchronize(dev)
     kms = a.elapsed_time(b) / KEV  # ms per launch
     plan_ms = None
+    hs_ms = None
+    if gap:  # the FindHalfSpaces kernel alone, same stream
+        a.record(stream)
+        for _ in range(20):
+            hs_step()
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        hs_ms = a.elapsed_time(b) / 20
+        kms = kms - hs_ms  # the QP kernel of the step
     if tick_cfg:  # the planning kernel alone, same stream
         a.record(stream)
         for _ in range(20):
@@ -472,10 +504,20 @@ def main():
             "parallelism": f"independent QP shards x{world} (no collective)"
                            + (f", scenario-aligned ({GROUP}) split of one global batch" if strong else ""),
             "solved_fraction": solved,
+            **({"step": "f110qp_find_half_spaces_dev (one 1,080-beam scan per QP) + f110qp_solve_batch_dev",
+                "halfspace_kernel_ms": hs_ms,
+                "halfspace_roofline": {"bound": "hbm", "bytes_per_scan": 4 * (ranges.shape[1] + 3 + 6 + 2),
+                                       "achieved_gbs": 4 * (ranges.shape[1] + 11) * Bper / (hs_ms * 1e-3) / 1e9,
+                                       "peak_gbs": HBM_PEAK_GBS,
+                                       "frac": 4 * (ranges.shape[1] + 11) * Bper / (hs_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+               if gap else {}),
             **({"plan_kernel_ms": plan_ms, "planned_fraction": float((pst.cpu().numpy() == 0).mean()),
                 "step": "f110qp_plan_batch_dev + f110qp_solve_batch_dev (x_ref_points = 50)"} if tick_cfg else {}),
             "mean_active_set_iters": float(itn.mean()),
             "max_active_set_iters": int(itn.max()),
+            **({"warm_key_hit_rate": key_hit,
+                "stream": "closed loop" if args.config != "c5_straight" else "straight (best case)"}
+               if stream_cfg else {}),
         },
         "roofline": {
             "bound": "hbm",

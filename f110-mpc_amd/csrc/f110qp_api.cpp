@@ -499,9 +499,10 @@ int f110qp_find_half_spaces_dev(int batch, const float* states, const float* ran
                                 float angle_min, float angle_inc, float angle_max,
                                 float ftg_thresh, float divider, float buffer, float* hs,
                                 int* gap_lo, int* gap_hi, void* stream) {
-  if (batch < 0 || nr <= 0) return fail(F110QP_ERR_INVALID, "bad batch / num_ranges");
+  if (batch < 0 || nr <= 0 || nr > 65535) return fail(F110QP_ERR_INVALID, "bad batch / num_ranges (1..65535)");
   if (batch == 0) return F110QP_OK;
   if (!states || !ranges || !hs) return fail(F110QP_ERR_INVALID, "NULL pointer argument");
+  if (!(angle_inc > 0.f)) return fail(F110QP_ERR_INVALID, "angle_increment must be > 0");
   hipError_t e = f110qp::launch_half_spaces(batch, states, ranges, nr, angle_min, angle_inc,
                                             angle_max, ftg_thresh, divider, buffer, hs, gap_lo,
                                             gap_hi, (hipStream_t)stream);

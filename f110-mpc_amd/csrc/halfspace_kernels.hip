@@ -1,20 +1,43 @@
 // halfspace_kernels.hip — batched Constraints::FindHalfSpaces (reference
-// src/constraints.cpp:116-265) on gfx950.
+// src/constraints.cpp:116-265) on gfx950: ONE WAVEFRONT PER SCAN.
 //
-// The reference walks one LaserScan sequentially with a small state machine whose quirks
-// (stale `hi` when a new gap opens, so single-beam gaps are never recorded; the (-1,-1)
-// "gap" recorded when the window opens on a short beam; int/float buffer comparison) decide
-// which gap wins. Those quirks make the winner depend on the scan order, so each scan is
-// processed by one lane exactly in reference order; the batch (one scan per candidate
-// scenario / QP) supplies the parallelism. The per-beam float arithmetic is written with
-// explicit round-to-nearest intrinsics so hipcc cannot contract it into FMAs that the x86
-// reference build does not use. Output is the f110qp_solve_batch half-space layout
-// hs[b] = (a1, b1, c1+0.5, a2, b2, c2+0.5) in float32.
+// The reference walks one LaserScan sequentially with a small state machine (lo, hi, in_gap,
+// max_gap) whose quirks decide which gap wins: a gap's `hi` is stale when the next gap opens, so
+// a single-beam gap is never recorded; the record is taken after every in-window beam with a
+// strict '>' (the first gap of the maximal length wins); and when the field-of-view window opens
+// on a short beam the initial (lo, hi) = (-1, -1) is recorded as a gap of length 0. Written
+// over the window's open beams (in window and range > ftg_thresh) that machine has a closed
+// form, which this kernel evaluates in parallel:
+//   * for an open beam p inside a run of open beams that started at s < p, the record compares
+//     p - s (for p = s the stale hi makes it negative); the answer is the FIRST beam p attaining
+//     the maximum of p - s, i.e. the end of the first longest run of >= 2 beams, (lo, hi) = (s, p);
+//   * with no run of >= 2 beams: (-1, -1) if the window's first beam is closed, else the
+//     initial (0, 0) (also when no beam falls in the window).
+// A wave streams its scan in 64-beam blocks (lane j loads beam 64 k + j: coalesced 256 B per
+// wave instruction, 8 blocks in flight per lane), turns the open flags into 64-bit ballots,
+// finds run starts with shifts of the ballot (the carry of block k-1's top beam included) and
+// the start of each lane's run as the highest start bit at or below it (or the last start of an
+// earlier block, a wave-uniform scalar). Each lane keeps the best key (p - s) << 16 | (65535 - p)
+// (larger run first, then the earlier beam); one wave max-reduction ends the scan. Lane 0 then
+// evaluates the endpoints and the two half-spaces with the reference's float/double types.
+// Every float operation uses explicit round-to-nearest intrinsics so hipcc cannot contract it
+// into FMAs the x86 reference build does not use. Output is the f110qp_solve_batch half-space
+// layout hs[b] = (a1, b1, c1+0.5, a2, b2, c2+0.5) in float32; a scan without a gap (the
+// reference reads ranges[-1] there) gives NaN.
 #include <hip/hip_runtime.h>
 
 #include "f110qp_kernels.h"
 
 namespace f110qp {
+
+constexpr int kHsWaves = 4;   // scans (waves) per 256-thread workgroup
+constexpr int kHsBatch = 8;   // 64-beam blocks loaded per lane before they are consumed
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
 
 __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __restrict__ states,
                                                          const float* __restrict__ ranges,
@@ -23,27 +46,63 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
                                                          float divider, float buffer,
                                                          float* __restrict__ hs, int* gap_lo,
                                                          int* gap_hi) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * kHsWaves + (threadIdx.x >> 6);
+  if (b >= B) return;  // whole waves only
   const float* r = ranges + (size_t)b * nr;
+  // num_scans = (angle_max - angle_min) / angle_increment + 1 in float, truncated (:118)
   int num_scans = (int)(__fadd_rn(__fdiv_rn(__fsub_rn(angle_max, angle_min), angle_inc), 1.0f));
   if (num_scans > nr) num_scans = nr;
-  int max_gap = -1, best_lo = 0, best_hi = 0, lo = -1, hi = -1;
-  bool in_gap = false;
-  const float lim = __fdiv_rn(1.571f, divider);
-  for (int ii = 0; ii < num_scans; ii++) {
-    const float angle = __fadd_rn(angle_min, __fmul_rn((float)ii, angle_inc));
-    if (angle > -lim && angle < lim) {
-      if (r[ii] > thresh) {
-        if (in_gap) hi = ii;
-        else { lo = ii; in_gap = true; }
-      } else {
-        in_gap = false;
+  const float lim = __fdiv_rn(1.571f, divider);  // :135
+  const int nblk = num_scans > 0 ? (num_scans + 63) / 64 : 0;
+  int best = -1;              // per-lane best key
+  int last_start = -1;        // last run start in the blocks before k (wave-uniform)
+  bool top_open = false;      // beam 64 k - 1 open (wave-uniform)
+  int w0 = -1;                // first in-window beam (wave-uniform)
+  bool w0_open = false;
+  for (int k0 = 0; k0 < nblk; k0 += kHsBatch) {
+    float v[kHsBatch];
+#pragma unroll
+    for (int j = 0; j < kHsBatch; j++) {
+      const int p = 64 * (k0 + j) + lane;
+      v[j] = p < num_scans ? r[p] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < kHsBatch; j++) {
+      const int k = k0 + j;
+      if (k >= nblk) break;
+      const int p = 64 * k + lane;
+      const float angle = __fadd_rn(angle_min, __fmul_rn((float)p, angle_inc));  // :133
+      const bool inwin = p < num_scans && angle > -lim && angle < lim;
+      const bool open = inwin && v[j] > thresh;  // :138
+      const unsigned long long W = __ballot(inwin), M = __ballot(open);
+      if (w0 < 0 && W) {
+        const int t = __builtin_ctzll(W);
+        w0 = 64 * k + t;
+        w0_open = (M >> t) & 1ull;
       }
-      if (hi - lo > max_gap) { max_gap = hi - lo; best_hi = hi; best_lo = lo; }
+      // run starts: open beams whose predecessor is not open
+      const unsigned long long S = M & ~((M << 1) | (top_open ? 1ull : 0ull));
+      const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+      const unsigned long long Sb = S & upto;
+      const int s = Sb ? 64 * k + 63 - __builtin_clzll(Sb) : last_start;
+      if (open && s < p) best = max(best, ((p - s) << 16) | (65535 - p));
+      if (S) last_start = 64 * k + 63 - __builtin_clzll(S);
+      top_open = (M >> 63) & 1ull;
     }
   }
-  if ((float)(best_hi - best_lo) > __fmul_rn(2.0f, buffer)) {
+  best = wave_max_i32(best);
+  if (lane != 0) return;
+  int best_lo, best_hi;
+  if (best >= 0) {
+    best_hi = 65535 - (best & 0xffff);
+    best_lo = best_hi - (best >> 16);
+  } else if (w0 >= 0 && !w0_open) {
+    best_lo = best_hi = -1;  // the initial (lo, hi) recorded on the window's first (short) beam
+  } else {
+    best_lo = best_hi = 0;
+  }
+  if ((float)(best_hi - best_lo) > __fmul_rn(2.0f, buffer)) {  // :173-177 (int vs float buffer_)
     best_hi = (int)((float)best_hi - buffer);
     best_lo = (int)((float)best_lo + buffer);
   }
@@ -59,12 +118,15 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   const float cur = states[3 * b + 2];
   const float ang1 = __fadd_rn(__fadd_rn(angle_min, __fmul_rn((float)best_lo, angle_inc)), cur);
   const float ang2 = __fadd_rn(__fadd_rn(angle_min, __fmul_rn((float)best_hi, angle_inc)), cur);
-  const float p1x = (float)__dadd_rn(__dmul_rn((double)r[best_lo], cos((double)ang1)), poseX);
-  const float p1y = (float)__dadd_rn(__dmul_rn((double)r[best_lo], sin((double)ang1)), poseY);
-  const float p2x = (float)__dadd_rn(__dmul_rn((double)r[best_hi], cos((double)ang2)), poseX);
-  const float p2y = (float)__dadd_rn(__dmul_rn((double)r[best_hi], sin((double)ang2)), poseY);
+  double s1, c1d, s2, c2d;
+  sincos((double)ang1, &s1, &c1d);
+  sincos((double)ang2, &s2, &c2d);
+  const float p1x = (float)__dadd_rn(__dmul_rn((double)r[best_lo], c1d), poseX);  // :181-185
+  const float p1y = (float)__dadd_rn(__dmul_rn((double)r[best_lo], s1), poseY);
+  const float p2x = (float)__dadd_rn(__dmul_rn((double)r[best_hi], c2d), poseX);
+  const float p2y = (float)__dadd_rn(__dmul_rn((double)r[best_hi], s2), poseY);
   const float px = (float)poseX, py = (float)poseY;
-  float a1 = __fsub_rn(py, p1y), b1 = __fsub_rn(p1x, px);
+  float a1 = __fsub_rn(py, p1y), b1 = __fsub_rn(p1x, px);  // :233-253
   float c1 = __fsub_rn(__fmul_rn(px, p1y), __fmul_rn(py, p1x));
   if (__fadd_rn(__fadd_rn(__fmul_rn(a1, p2x), __fmul_rn(b1, p2y)), c1) < 0.f) {
     a1 = -a1; b1 = -b1; c1 = -c1;
@@ -74,7 +136,7 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   if (__fadd_rn(__fadd_rn(__fmul_rn(a2, p1x), __fmul_rn(b2, p1y)), c2) < 0.f) {
     a2 = -a2; b2 = -b2; c2 = -c2;
   }
-  o[0] = a1; o[1] = b1; o[2] = (float)((double)c1 + 0.5);
+  o[0] = a1; o[1] = b1; o[2] = (float)((double)c1 + 0.5);  // :255-264
   o[3] = a2; o[4] = b2; o[5] = (float)((double)c2 + 0.5);
 }
 
@@ -83,8 +145,7 @@ hipError_t launch_half_spaces(int B, const float* states, const float* ranges, i
                               float divider, float buffer, float* hs, int* gap_lo, int* gap_hi,
                               hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  const int threads = 256;
-  hipLaunchKernelGGL(half_space_kernel, dim3((B + threads - 1) / threads), dim3(threads), 0, s,
+  hipLaunchKernelGGL(half_space_kernel, dim3((B + kHsWaves - 1) / kHsWaves), dim3(64 * kHsWaves), 0, s,
                      B, states, ranges, nr, angle_min, angle_inc, angle_max, thresh, divider,
                      buffer, hs, gap_lo, gap_hi);
   return hipGetLastError();

@@ -133,6 +133,66 @@ def make_stream(batch: int, horizon: int, ticks: int, seed: int = 0, dt: float =
     return ticks_out
 
 
+def simulate_dynamics(x, u, dt=0.01):
+    """Model::simulate_dynamics (src/model.cpp:61-75, CAR_LENGTH = 0.35), vectorised fp64:
+    x [B,3] (x, y, ori), u [B,2] (v, steer) -> the state one Euler step later."""
+    x = np.asarray(x, np.float64)
+    u = np.asarray(u, np.float64)
+    d = np.stack([u[:, 0] * np.cos(x[:, 2]), u[:, 0] * np.sin(x[:, 2]), np.tan(u[:, 1]) * u[:, 0] / CAR_LENGTH], 1)
+    return x + d * dt
+
+
+def closed_loop_stream(solve, batch: int, horizon: int, ticks: int, seed: int = 0, dt: float = 0.01,
+                       replan_every: int = 5, lateral: float = 0.3, steer_range: float = 0.4):
+    """Config C5 as a closed receding-horizon loop (project::OdomCallback's MPC branch,
+    src/project.cpp:160-198, driven by a simulated car). Per tick and car:
+      - x0 = the car's pose (x, y, GetCarOrientation), so theta0 changes every tick;
+      - u_lin = GetNextInput() with v forced to 4.5 (project.cpp:163-170): the steer of the
+        previous solution's next input u*_1 (u*_0 is applied first);
+      - x_ref = the first N states of the car's current mini path; the path is re-planned from the
+        current pose every `replan_every` ticks (the reference re-plans within 1.98 m of the end
+        of its 2.2 m mini path, project.cpp:180-188), staggered over the cars;
+      - then the plant advances: x0 <- simulate_dynamics(x0, u*_0, dt) (model.cpp:61-75).
+    `solve(x0, u_lin, x_ref) -> u [B, N, 2]` is the solver that closes the loop (a GPU back end or
+    the oracle). Returns the list of tick dicts (x0, u_lin, x_ref), float32 ABI layouts."""
+    rng = np.random.default_rng(seed)
+    base = make_batch(batch, horizon, seed=seed, lateral=lateral, steer_range=steer_range)
+    x = base["x0"].astype(np.float64)
+    ul = base["u_lin"].copy()
+    xr = base["x_ref"].copy()
+    out = []
+    for t in range(ticks):
+        if t > 0:
+            rp = (np.arange(batch) + t) % replan_every == 0
+            n = int(rp.sum())
+            if n:
+                x0f = x[rp].astype(np.float32)
+                path = mini_paths(rng.uniform(-steer_range, steer_range, n))
+                xr[rp] = _to_ref(path, rng.uniform(-lateral, lateral, n), x0f, horizon, "zero")
+        x0 = x.astype(np.float32)
+        tick = dict(x0=x0, u_lin=ul.copy(), x_ref=xr.copy())
+        out.append(tick)
+        u = np.asarray(solve(tick["x0"], tick["u_lin"], tick["x_ref"]), np.float64)
+        ok = np.isfinite(u).all(axis=(1, 2))
+        u0 = np.where(ok[:, None], u[:, 0], np.stack([np.full(batch, 0.5), np.zeros(batch)], 1))  # Input(0.5, 0)
+        x = simulate_dynamics(x, u0, dt)
+        nxt = u[:, 1] if horizon > 1 else u[:, 0]
+        ul = np.stack([np.full(batch, SPEED), np.where(ok, nxt[:, 1], ul[:, 1])], 1).astype(np.float32)
+    return out
+
+
+def warm_key_hit_rate(ticks) -> float:
+    """Fraction of (car, tick > 0) whose linearisation point bits (theta0, v, steer) equal the
+    previous tick's: the wave back end's warm W = H^-1 cache hits exactly then."""
+    hits = tot = 0
+    for a, b in zip(ticks[:-1], ticks[1:]):
+        same = (a["x0"][:, 2].view(np.uint32) == b["x0"][:, 2].view(np.uint32)) & \
+               (a["u_lin"].view(np.uint32) == b["u_lin"].view(np.uint32)).all(axis=1)
+        hits += int(same.sum())
+        tot += same.size
+    return hits / max(1, tot)
+
+
 # ---- planning scenes (pose + LaserScan + global path) for the device planning stage -----------
 
 def track_waypoints(n: int = 500, a: float = 12.0, b: float = 6.0) -> np.ndarray:

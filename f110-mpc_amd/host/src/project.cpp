@@ -1,6 +1,7 @@
 // project — the reference node's control logic (src/project.cpp) without ROS.
 #include "f110mpc/project.h"
 
+#include <chrono>
 #include <cstdio>
 
 #include "f110qp.h"
@@ -14,6 +15,8 @@ Project::Project(const Params& p, const std::vector<State>& global_path)
     wp_.push_back(s.y());
   }
 }
+
+Project::~Project() { StopDriveLoop(); }
 
 void Project::ScanCallback(const LaserScan& scan) {
   if (!first_pose_estimate_) return;  // :43
@@ -80,21 +83,40 @@ void Project::OdomCallback(const Pose& pose) {
   // with an emptied miniPath the reference reads past its end (CreateGradientVector); here
   // MPC::Update refuses a path shorter than the horizon and keeps its previous solution
   mpc_.Update(current_state, input, miniPath_);  // :190
-  current_inputs_ = mpc_.solved_trajectory();    // :192
-  inputs_idx_ = 0;
+  inputs_.Publish(mpc_.solved_trajectory());     // :192-193, atomically with inputs_idx_ = 0
 }
 
 Input Project::GetNextInput() {
-  if (inputs_idx_ >= current_inputs_.size()) {
-    std::fprintf(stderr, "ran out of QP soln\n");  // :210-213
-    return Input(0.5, 0.0);
-  }
-  return current_inputs_[inputs_idx_];
+  bool ran_out = false;
+  const Input in = inputs_.Peek(&ran_out);
+  if (ran_out) std::fprintf(stderr, "ran out of QP soln\n");  // :210-213
+  return in;
 }
 
 bool Project::DriveStep(Input* out) {
   if (!(first_pose_estimate_ && first_scan_estimate_)) return false;  // :221
-  *out = GetNextInput();
-  inputs_idx_++;  // :233
+  *out = inputs_.Take();  // GetNextInput() + inputs_idx_++ (:224-233) in one critical section
   return true;
+}
+
+void Project::StartDriveLoop(std::function<void(const Input&)> publish, int period_ms) {
+  StopDriveLoop();
+  if (period_ms < 0) period_ms = static_cast<int>(2 * params_.dt * 1000);  // :233 int dt_ms
+  drive_run_ = true;
+  drive_thread_ = std::thread([this, publish, period_ms] {
+    while (drive_run_) {
+      Input in;
+      if (DriveStep(&in)) {
+        publish(in);  // drive_pub_.publish(drive_msg) (:226-231)
+        std::this_thread::sleep_for(std::chrono::milliseconds(period_ms));
+      } else {
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+    }
+  });
+}
+
+void Project::StopDriveLoop() {
+  drive_run_ = false;
+  if (drive_thread_.joinable()) drive_thread_.join();
 }

@@ -16,6 +16,9 @@
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <chrono>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "f110mpc/mpc.h"
@@ -162,7 +165,71 @@ static int project(const char* params_path, const char* in, const char* out) {
   return 0;
 }
 
+// The scripted drive with the DriveLoop thread running (Project::StartDriveLoop, 1 ms period)
+// while the callbacks run on this thread: every published input must be an element of one of the
+// solutions MPC::Update produced (or the Input(0.5, 0) fallback). Prints a JSON summary.
+static int project_threaded(const char* params_path, const char* in) {
+  Params p;
+  if (!LoadParams(params_path, &p)) return 2;
+  std::ifstream f(in, std::ios::binary);
+  f.seekg(0, std::ios::end);
+  const size_t n = static_cast<size_t>(f.tellg()) / 8;
+  f.seekg(0);
+  std::vector<double> v(n);
+  f.read(reinterpret_cast<char*>(v.data()), n * 8);
+  const int T = static_cast<int>(v[0]), R = static_cast<int>(v[1]), W = static_cast<int>(v[2]);
+  LaserScan scan;
+  scan.angle_min = static_cast<float>(v[3]);
+  scan.angle_increment = static_cast<float>(v[4]);
+  scan.angle_max = static_cast<float>(v[5]);
+  size_t o = 6;
+  std::vector<State> path;
+  for (int i = 0; i < W; i++, o += 2) path.emplace_back(v[o], v[o + 1], 0.0);
+  Project prj(p, path);
+  std::mutex mu;
+  std::vector<Input> published;
+  prj.StartDriveLoop([&](const Input& in) {
+    std::lock_guard<std::mutex> lk(mu);
+    published.push_back(in);
+  }, 1);
+  std::vector<std::vector<Input>> solutions;
+  for (int t = 0; t < T; t++) {
+    Pose pose;
+    pose.x = v[o]; pose.y = v[o + 1]; pose.qz = v[o + 2]; pose.qw = v[o + 3];
+    o += 4;
+    scan.ranges.assign(R, 0.f);
+    for (int r = 0; r < R; r++) scan.ranges[r] = static_cast<float>(v[o + r]);
+    o += R;
+    prj.OdomCallback(pose);
+    prj.ScanCallback(scan);
+    solutions.push_back(prj.current_inputs());
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  }
+  prj.StopDriveLoop();
+  long ok = 0, fallback = 0, bad = 0;
+  for (const Input& in : published) {
+    bool found = in.v() == 0.5 && in.steer_ang() == 0.0;
+    fallback += found;
+    for (size_t s = 0; s < solutions.size() && !found; s++)
+      for (const Input& u : solutions[s])
+        if (u.v() == in.v() && u.steer_ang() == in.steer_ang()) { found = true; break; }
+    ok += found;
+    bad += !found;
+  }
+  int changes = 0;
+  for (size_t s = 1; s < solutions.size(); s++) {
+    bool same = solutions[s].size() == solutions[s - 1].size();
+    for (size_t k = 0; same && k < solutions[s].size(); k++)
+      same = solutions[s][k].v() == solutions[s - 1][k].v() && solutions[s][k].steer_ang() == solutions[s - 1][k].steer_ang();
+    changes += !same;
+  }
+  std::printf("{\"published\": %zu, \"from_solutions\": %ld, \"fallback\": %ld, \"unknown\": %ld, \"new_solutions\": %d}\n",
+              published.size(), ok - fallback, fallback, bad, changes);
+  return bad == 0 ? 0 : 3;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 4 && !std::strcmp(argv[1], "project_threaded")) return project_threaded(argv[2], argv[3]);
   if (argc >= 5 && !std::strcmp(argv[1], "project")) return project(argv[2], argv[3], argv[4]);
   if (argc >= 3 && !std::strcmp(argv[1], "cpu")) return cpu(argv[2]);
   if (argc >= 5 && !std::strcmp(argv[1], "tick")) return tick(argv[2], argv[3], argv[4], false);

@@ -171,7 +171,8 @@ int f110qp_find_half_spaces(const double state[3], const float* ranges, int num_
                             float ftg_thresh, float divider, float buffer, double l1[3],
                             double l2[3]);
 
-/* Batched FindHalfSpaces on the device: scans [B][num_ranges], states [B][3] -> hs [B][2][3]
+/* Batched FindHalfSpaces on the device, one wavefront per scan (num_ranges <= 65535, angle_increment
+ * > 0): scans [B][num_ranges], states [B][3] -> hs [B][2][3]
  * (float32, the f110qp_solve_batch halfspace layout); gap_lo/gap_hi [B] may be NULL. */
 int f110qp_find_half_spaces_dev(int batch, const float* states, const float* ranges,
                                 int num_ranges, float angle_min, float angle_increment,

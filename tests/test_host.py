@@ -191,3 +191,23 @@ def test_project_callbacks_drive_the_tick(demo, oracle, tmp_path):
             assert abs(got[5] - exp[5]) <= 1e-4 * max(1.0, abs(exp[5])) and abs(got[6] - exp[6]) <= 1e-4, (t, got[5:7], exp[5:7])
     # plan, two MPC ticks, then the 1.98 m trigger clears the path: ~2 solves per 4 ticks
     assert replans >= 2 and (res[:, 4] == 1).sum() >= T // 3
+
+
+@pytest.mark.gpu
+def test_project_drive_loop_thread(demo, tmp_path):
+    """F3: Project::StartDriveLoop runs the reference's DriveLoop (src/project.cpp:217-236) on
+    its own thread (1 ms period) while the callbacks solve on the caller's thread: every
+    published input is an element of a solution MPC::Update produced or the Input(0.5, 0)
+    fallback (no torn or stale-index reads), and new solutions keep arriving."""
+    T = 60
+    d = workload.drive_stream(T, seed=5)
+    R = d["ranges"].shape[1]
+    W = d["waypoints"].shape[0]
+    header = np.array([T, R, W, d["angle_min"], d["angle_inc"], d["angle_max"]], np.float64)
+    body = [d["waypoints"][:, :2].ravel()]
+    for t in range(T):
+        body += [d["pose"][t], d["ranges"][t].astype(np.float64)]
+    inp = tmp_path / "prj.bin"
+    np.concatenate([header] + body).astype(np.float64).tofile(inp)
+    out = json.loads(subprocess.check_output([demo, "project_threaded", PARAMS, str(inp)], timeout=120))
+    assert out["unknown"] == 0 and out["published"] > T and out["from_solutions"] > 0 and out["new_solutions"] >= 5
