@@ -14,14 +14,16 @@
 //   * with no run of >= 2 beams: (-1, -1) if the window's first beam is closed, else the
 //     initial (0, 0) (also when no beam falls in the window).
 // A wave streams its scan in 64-beam blocks (lane j loads beam 64 k + j: coalesced 256 B per
-// wave instruction, 8 blocks in flight per lane), turns the open flags into 64-bit ballots,
+// wave instruction; a 1,080-beam scan is one round trip, every block in flight at once), turns the open flags into 64-bit ballots,
 // finds run starts with shifts of the ballot (the carry of block k-1's top beam included) and
 // the start of each lane's run as the highest start bit at or below it (or the last start of an
 // earlier block, a wave-uniform scalar). Each lane keeps the best key (p - s) << 16 | (65535 - p)
 // (larger run first, then the earlier beam); one wave max-reduction ends the scan. Lane 0 then
 // evaluates the endpoints and the two half-spaces with the reference's float/double types.
-// Every float operation uses explicit round-to-nearest intrinsics so hipcc cannot contract it
-// into FMAs the x86 reference build does not use. Output is the f110qp_solve_batch half-space
+// FP contraction is off for the whole kernel body (hipcc fuses a*b+c into an FMA by default and
+// does so even through the __fmul_rn/__fadd_rn helpers, which are plain operators inlined from
+// the HIP headers; the x86 reference build does not fuse: with fusion 18% of the end points came
+// out one float ulp off), so the reference's float/double expressions are written as they are. Output is the f110qp_solve_batch half-space
 // layout hs[b] = (a1, b1, c1+0.5, a2, b2, c2+0.5) in float32; a scan without a gap (the
 // reference reads ranges[-1] there) gives NaN.
 #include <hip/hip_runtime.h>
@@ -31,7 +33,7 @@
 namespace f110qp {
 
 constexpr int kHsWaves = 4;   // scans (waves) per 256-thread workgroup
-constexpr int kHsBatch = 8;   // 64-beam blocks loaded per lane before they are consumed
+constexpr int kHsBatch = 24;  // 64-beam blocks loaded per lane before they are consumed (1,536 beams)
 
 __device__ __forceinline__ int wave_max_i32(int v) {
 #pragma unroll
@@ -46,14 +48,15 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
                                                          float divider, float buffer,
                                                          float* __restrict__ hs, int* gap_lo,
                                                          int* gap_hi) {
+#pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * kHsWaves + (threadIdx.x >> 6);
   if (b >= B) return;  // whole waves only
   const float* r = ranges + (size_t)b * nr;
   // num_scans = (angle_max - angle_min) / angle_increment + 1 in float, truncated (:118)
-  int num_scans = (int)(__fadd_rn(__fdiv_rn(__fsub_rn(angle_max, angle_min), angle_inc), 1.0f));
+  int num_scans = (int)((angle_max - angle_min) / angle_inc + 1.0f);
   if (num_scans > nr) num_scans = nr;
-  const float lim = __fdiv_rn(1.571f, divider);  // :135
+  const float lim = 1.571f / divider;  // :135
   const int nblk = num_scans > 0 ? (num_scans + 63) / 64 : 0;
   int best = -1;              // per-lane best key
   int last_start = -1;        // last run start in the blocks before k (wave-uniform)
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
       const int k = k0 + j;
       if (k >= nblk) break;
       const int p = 64 * k + lane;
-      const float angle = __fadd_rn(angle_min, __fmul_rn((float)p, angle_inc));  // :133
+      const float angle = angle_min + (float)p * angle_inc;  // :133
       const bool inwin = p < num_scans && angle > -lim && angle < lim;
       const bool open = inwin && v[j] > thresh;  // :138
       const unsigned long long W = __ballot(inwin), M = __ballot(open);
@@ -92,7 +95,8 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
     }
   }
   best = wave_max_i32(best);
-  if (lane != 0) return;
+  // The tail runs on every lane with the same values (a partially masked wave runs ~2.4x slower
+  // on a loaded CU, tools/microbench/contention.hip); lane 0 stores.
   int best_lo, best_hi;
   if (best >= 0) {
     best_hi = 65535 - (best & 0xffff);
@@ -102,42 +106,47 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   } else {
     best_lo = best_hi = 0;
   }
-  if ((float)(best_hi - best_lo) > __fmul_rn(2.0f, buffer)) {  // :173-177 (int vs float buffer_)
+  if ((float)(best_hi - best_lo) > 2.0f * buffer) {  // :173-177 (int vs float buffer_)
     best_hi = (int)((float)best_hi - buffer);
     best_lo = (int)((float)best_lo + buffer);
   }
-  if (gap_lo) gap_lo[b] = best_lo;
-  if (gap_hi) gap_hi[b] = best_hi;
+  if (lane == 0 && gap_lo) gap_lo[b] = best_lo;
+  if (lane == 0 && gap_hi) gap_hi[b] = best_hi;
   float* o = hs + (size_t)b * 6;
-  if (best_lo < 0 || best_hi < 0 || best_lo >= nr || best_hi >= nr) {
+  if (best_lo < 0 || best_hi < 0 || best_lo >= nr || best_hi >= nr) {  // wave-uniform
     const float nanv = __int_as_float(0x7fc00000);
-    for (int j = 0; j < 6; j++) o[j] = nanv;
+    if (lane == 0)
+      for (int j = 0; j < 6; j++) o[j] = nanv;
     return;
   }
   const double poseX = (double)states[3 * b + 0], poseY = (double)states[3 * b + 1];
   const float cur = states[3 * b + 2];
-  const float ang1 = __fadd_rn(__fadd_rn(angle_min, __fmul_rn((float)best_lo, angle_inc)), cur);
-  const float ang2 = __fadd_rn(__fadd_rn(angle_min, __fmul_rn((float)best_hi, angle_inc)), cur);
-  double s1, c1d, s2, c2d;
-  sincos((double)ang1, &s1, &c1d);
-  sincos((double)ang2, &s2, &c2d);
-  const float p1x = (float)__dadd_rn(__dmul_rn((double)r[best_lo], c1d), poseX);  // :181-185
-  const float p1y = (float)__dadd_rn(__dmul_rn((double)r[best_lo], s1), poseY);
-  const float p2x = (float)__dadd_rn(__dmul_rn((double)r[best_hi], c2d), poseX);
-  const float p2y = (float)__dadd_rn(__dmul_rn((double)r[best_hi], s2), poseY);
+  const float ang1 = angle_min + (float)best_lo * angle_inc + cur;  // :179-180
+  const float ang2 = angle_min + (float)best_hi * angle_inc + cur;
+  // even lanes evaluate the first end point's cos/sin, odd lanes the second (::cos/::sin(double))
+  double sl, cl;
+  sincos((double)((lane & 1) ? ang2 : ang1), &sl, &cl);
+  const double s1 = __shfl(sl, 0), c1d = __shfl(cl, 0);
+  const double s2 = __shfl(sl, 1), c2d = __shfl(cl, 1);
+  const float p1x = (float)((double)r[best_lo] * c1d + poseX);  // :181-185
+  const float p1y = (float)((double)r[best_lo] * s1 + poseY);
+  const float p2x = (float)((double)r[best_hi] * c2d + poseX);
+  const float p2y = (float)((double)r[best_hi] * s2 + poseY);
   const float px = (float)poseX, py = (float)poseY;
-  float a1 = __fsub_rn(py, p1y), b1 = __fsub_rn(p1x, px);  // :233-253
-  float c1 = __fsub_rn(__fmul_rn(px, p1y), __fmul_rn(py, p1x));
-  if (__fadd_rn(__fadd_rn(__fmul_rn(a1, p2x), __fmul_rn(b1, p2y)), c1) < 0.f) {
+  float a1 = py - p1y, b1 = p1x - px;  // :233-253
+  float c1 = px * p1y - py * p1x;
+  if (a1 * p2x + b1 * p2y + c1 < 0.f) {
     a1 = -a1; b1 = -b1; c1 = -c1;
   }
-  float a2 = __fsub_rn(py, p2y), b2 = __fsub_rn(p2x, px);
-  float c2 = __fsub_rn(__fmul_rn(px, p2y), __fmul_rn(py, p2x));
-  if (__fadd_rn(__fadd_rn(__fmul_rn(a2, p1x), __fmul_rn(b2, p1y)), c2) < 0.f) {
+  float a2 = py - p2y, b2 = p2x - px;
+  float c2 = px * p2y - py * p2x;
+  if (a2 * p1x + b2 * p1y + c2 < 0.f) {
     a2 = -a2; b2 = -b2; c2 = -c2;
   }
-  o[0] = a1; o[1] = b1; o[2] = (float)((double)c1 + 0.5);  // :255-264
-  o[3] = a2; o[4] = b2; o[5] = (float)((double)c2 + 0.5);
+  if (lane == 0) {
+    o[0] = a1; o[1] = b1; o[2] = (float)((double)c1 + 0.5);  // :255-264
+    o[3] = a2; o[4] = b2; o[5] = (float)((double)c2 + 0.5);
+  }
 }
 
 hipError_t launch_half_spaces(int B, const float* states, const float* ranges, int nr,

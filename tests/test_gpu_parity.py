@@ -258,7 +258,33 @@ def test_half_space_kernel_adversarial(oracle, capi, cuda, nr, seed):
             assert np.isnan(hs[b]).all()
             continue
         ref = np.float32([l1, l2])
-        np.testing.assert_allclose(hs[b], ref, rtol=2e-6, atol=2e-6 * np.abs(ref).max())
+        if not np.isfinite(ref).all():  # an infinite range at an end point: inf/NaN propagate alike
+            np.testing.assert_array_equal(np.isnan(hs[b]), np.isnan(ref))
+            inf = np.isinf(ref)
+            np.testing.assert_array_equal(hs[b][inf], ref[inf])
+            continue
+        # fp32 rounding of the reference's float arithmetic (constraints.cpp:233-253) from end
+        # points whose cos/sin may differ by one double ulp between libms: a, b carry the end
+        # point's float ulp, c = px*p1y - py*p1x the ulp of the products (cancellation)
+        P = max(abs(float(st[b, 0])), abs(float(st[b, 1]))) + max(float(r[b, rlo]), float(r[b, rhi]))
+        eps = float(np.finfo(np.float32).eps)
+        tol = np.float64([8 * eps * P, 8 * eps * P, 8 * eps * 2 * P * P])
+        for k in range(2):
+            if (np.abs(hs[b][k].astype(np.float64) - ref[k]) <= tol).all():
+                continue
+            # orientation flip (constraints.cpp:236,248): allowed only where the side test
+            # a*px + b*py + c of the other end point is zero to rounding (coincident or collinear
+            # end points), where a 1-ulp cos/sin difference decides the sign
+            flip = np.float32([-ref[k][0], -ref[k][1], 1.0 - ref[k][2]])  # (-a, -b, -c + 0.5)
+            assert (np.abs(hs[b][k].astype(np.float64) - flip) <= tol).all(), (b, k, hs[b], ref, tol)
+            ang = [np.float32(np.float32(amin + np.float32(np.float32(i) * ainc)) + st[b, 2]) for i in (rlo, rhi)]
+            p1 = [np.float64(r[b, rlo]) * np.cos(np.float64(ang[0])) + st[b, 0], np.float64(r[b, rlo]) * np.sin(np.float64(ang[0])) + st[b, 1]]
+            p2 = [np.float64(r[b, rhi]) * np.cos(np.float64(ang[1])) + st[b, 0], np.float64(r[b, rhi]) * np.sin(np.float64(ang[1])) + st[b, 1]]
+            q = p2 if k == 0 else p1
+            a_, b_, c_ = (float(v) for v in ref[k])
+            c_ -= 0.5
+            side = a_ * q[0] + b_ * q[1] + c_
+            assert abs(side) <= 1e-5 * (abs(a_ * q[0]) + abs(b_ * q[1]) + abs(c_)), (b, k, side)
         same += int((hs[b] == ref).all())
         total += 1
     assert total == 0 or same / total >= 0.9, (same, total)
@@ -586,4 +612,4 @@ def test_closed_loop_stream_warm(oracle, capi, be):
         itc.append(cold.solve(w["x0"], w["u_lin"], w["x_ref"])[3].mean())
     warm.close()
     cold.close()
-    assert np.mean(itw[1:]) <= np.mean(itc[1:]) + 1e-9
+    assert np.mean(itw[1:]) <= np.mean(itc[1:]) + 1e-9, (np.mean(itw[1:]), np.mean(itc[1:]))
