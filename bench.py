@@ -87,7 +87,9 @@ def load_traffic(config: str, batch: int, horizon: int, backend: str):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary of this config
     (tools/profile_round.sh + tools/summarize_profiles.py), only when it was taken on the same
     (config, batch, horizon, back end); None otherwise."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}_{batch}.json")
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None
     try:

@@ -66,9 +66,9 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   for (int k0 = 0; k0 < nblk; k0 += kHsBatch) {
     float v[kHsBatch];
 #pragma unroll
-    for (int j = 0; j < kHsBatch; j++) {
+    for (int j = 0; j < kHsBatch; j++) {  // unconditional loads (clamped index): no exec masking
       const int p = 64 * (k0 + j) + lane;
-      v[j] = p < num_scans ? r[p] : 0.f;
+      v[j] = r[p < num_scans ? p : num_scans - 1];
     }
 #pragma unroll
     for (int j = 0; j < kHsBatch; j++) {

@@ -4,7 +4,8 @@ For each config: the kernel-stats CSV of the trace pass is copied; the PMC passe
 FETCH_SIZE and WRITE_SIZE (KB per dispatch) of the dominant kernel, averaged over its
 dispatches, reported raw (see MI355X_MICROARCH.md: gfx950 FETCH_SIZE under-reports wide
 coalesced streams by 2x; these kernels' reads are narrow gathers, so no correction is applied).
-Usage: python tools/summarize_profiles.py r01 c2 c4 ...
+Usage: python tools/summarize_profiles.py r02 c2 c4 c4_8192 ... (a name <config>_<batch> is the
+config run at that batch, profiled with PROF_NAME=<name> tools/profile_round.sh <config> --batch <batch>)
 """
 import csv
 import glob
@@ -61,7 +62,7 @@ def main():
         B = bench["config"]["batch_per_gpu"]
         hbm = (fetch + write) * 1024 if fetch is not None and write is not None else None
         out = {
-            "config": c.split("@")[0],
+            "config": c.split("_")[0] if c.split("_")[-1].isdigit() else c,
             "batch": B,
             "horizon": bench["config"]["horizon"],
             "backend": be,
