@@ -381,10 +381,19 @@ def main():
     def hs_step():
         capi.find_half_spaces_dev(x0, rng_d, amin, ainc, amax, hs, stream=stream)
 
+    # the static-buffer steps go through a prepared launcher: one C call per step, as a C++
+    # caller of the ABI would make (Python argument marshalling is not part of the solve)
+    fast = None
+    if not (tick_cfg or stream_cfg):
+        fast = (solver.prepare_grouped_dev(x0, ul, xr, hs, gid, ngroups, uo, xo, st, it, stream=stream) if grouped
+                else solver.prepare_dev(x0, ul, xr, hs, uo, xo, st, it, stream=stream))
+
     def step():
         if gap:
             hs_step()
-        if tick_cfg:
+        if fast is not None:
+            fast()
+        elif tick_cfg:
             plan_step()
             # scenarios without a valid candidate keep NaN x_ref and come back non-solved,
             # as MPC::Update is skipped for them in the reference (project.cpp:117-121)

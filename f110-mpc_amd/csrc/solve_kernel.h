@@ -830,12 +830,10 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       }
     }
     wsync();
-    if constexpr (!GAP) {
 #pragma unroll
-      for (int r = 0; r < R; r++)
+    for (int r = 0; r < R; r++)
 #pragma unroll
-        for (int j = 0; j < NUM; j++) hrow[r][j] = (vv[r] < NUM) ? -sm.W[j][vv[r]] : 0.f;
-    }
+      for (int j = 0; j < NUM; j++) hrow[r][j] = (vv[r] < NUM) ? -sm.W[j][vv[r]] : 0.f;
   } else {
   // ---- 2b. condensed Hessian rows (closed form, fp32) -------------------------------------
   // Row v = (k, a), column w = (l, b). For l <= k the stages that see both inputs are
@@ -966,7 +964,9 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   // rollout and costate, correction through T on F) and re-checked exactly; a violated row
   // hands the set over to the GI loop below as a valid GI state (independent normals,
   // positive multipliers). No convergence within P.pdas_max passes (10) -> plain GI from the
-  // unconstrained point.
+  // unconstrained point. (Measured and not kept for the gap-row kernel: the same box PDAS first,
+  // then GI from its set for the violated gap rows: C3 327 -> 451 us, the GI steps are the gap
+  // rows themselves and the extra code halves that kernel's occupancy.)
   if constexpr (!GAP) {
     if (status == F110QP_SOLVED_ID) {
       STAMP(t_pdas);
@@ -1064,13 +1064,32 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           wave_argmin(adx, dummy);  // -max |dx|
           if (-adx <= 1e-5f) break;
         }
-        // exact feasibility re-check of the free variables at the refined point
+        // exact re-check at the refined point, in fp64: the box rows of the free variables and
+        // the sign of the active bounds' multipliers r1 = (H u + g)_A (lower bound: r1 >= 0,
+        // upper: r1 <= 0; the fp32 PDAS decided them)
+        double r1f[R];
+        rollout_f64<R>(M, lane, u64, px, py, th);
+        grad_f64<R>(M, P, lane, N, u64, px, py, th, rxd, ryd, rthd, zero, zero, r1f);
+        float gmax = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; r++) gmax = fmaxf(gmax, valid[r] ? fabsf(gr[r]) : 0.f);
+        {
+          int dummy = 0;
+          gmax = -gmax;
+          wave_argmin(gmax, dummy);
+          gmax = -gmax;
+        }
+        const double dtol = 1e-6 * (1.0 + (double)gmax);
+        bool dual_bad = false;
         float best64 = 0.f, sp64 = 0.f;
         int bid64 = 0x7fffffff;
 #pragma unroll
         for (int r = 0; r < R; r++) {
-          if (!valid[r] || act[r]) continue;
+          if (!valid[r]) continue;
           const int v = vv[r];
+          if (act[r] == 1 && r1f[r] < -dtol) dual_bad = true;
+          if (act[r] == 2 && r1f[r] > dtol) dual_bad = true;
+          if (act[r]) continue;
           const double s0 = u64[r] - (double)lb[r], s1 = (double)ub[r] - u64[r];
           const float v0 = (float)(s0 / (1.0 + fabs((double)lb[r])));
           const float v1 = (float)(s1 / (1.0 + fabs((double)ub[r])));
@@ -1078,10 +1097,15 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           if (v1 < -1e-9f && v1 < best64) { best64 = v1; bid64 = 3 * v + 1; sp64 = (float)s1; }
         }
         wave_argmin(best64, bid64);
+        dual_bad = __ballot(dual_bad) != 0ull;
 #pragma unroll
         for (int r = 0; r < R; r++) actf[r] = act[r];  // bit0 lower, bit1 upper
         STAMP_ACC(acc_refine, t_ref0);
-        if (bid64 == 0x7fffffff) {
+        if (dual_bad) {
+          // a wrong-sign multiplier: the set is not optimal; plain GI from the unconstrained point
+#pragma unroll
+          for (int r = 0; r < R; r++) actf[r] = 0;
+        } else if (bid64 == 0x7fffffff) {
           final_ok = true;
         } else {
           // hand the set to the GI state: slots, chol(S_A), multipliers, the violated row

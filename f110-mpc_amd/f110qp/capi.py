@@ -225,6 +225,41 @@ class Solver:
                                                _tp(u_out), _tp(x_out), _tp(status), _tp(iters),
                                                C.c_void_p(stream.cuda_stream)), "f110qp_solve_batch_dev")
 
+    def prepare_dev(self, x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters=None, stream=None):
+        """A launcher for repeated f110qp_solve_batch_dev calls on the same device buffers: the
+        ctypes arguments are converted once, each call is one C call (what a C++ caller of the ABI
+        pays; bench.py's timed steps use it so Python argument marshalling is not the step)."""
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream(x0.device)
+        fn = self.lib.f110qp_solve_batch_dev
+        args = (self._h, x0.shape[0], _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace), _tp(u_out), _tp(x_out),
+                _tp(status), _tp(iters), C.c_void_p(stream.cuda_stream))
+
+        def launch():
+            rc = fn(*args)
+            if rc != OK:
+                _check(rc, "f110qp_solve_batch_dev")
+        return launch
+
+    def prepare_grouped_dev(self, x0, u_lin, x_ref, halfspace, group, num_groups, u_out, x_out, status,
+                            iters=None, stream=None):
+        """prepare_dev for f110qp_solve_grouped_dev."""
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream(x0.device)
+        fn = self.lib.f110qp_solve_grouped_dev
+        args = (self._h, x0.shape[0], _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace), _tp(group), int(num_groups),
+                _tp(u_out), _tp(x_out), _tp(status), _tp(iters), C.c_void_p(stream.cuda_stream))
+
+        def launch():
+            rc = fn(*args)
+            if rc != OK:
+                _check(rc, "f110qp_solve_grouped_dev")
+        return launch
+
     def solve_grouped(self, x0, u_lin, x_ref, group, num_groups=None, halfspace=None):
         """Grouped solve on host arrays (f110qp_solve_grouped): group [B] int scenario ids."""
         N = self.horizon

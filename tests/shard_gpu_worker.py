@@ -1,0 +1,48 @@
+"""One rank of the multi-process HIP shard check (tests/test_gpu_shard.py): launched by
+torch.distributed.run with the gloo backend; every rank solves its scenario-aligned shard of a
+C4-style grouped batch on cuda:0 through the C ABI (f110qp_solve_grouped_dev, the back end given),
+the shards are all-gathered over gloo (host tensors), rank 0 writes the global result."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "f110-mpc_amd"))
+from f110qp import capi, workload  # noqa: E402
+from f110qp.shard import solve_sharded  # noqa: E402
+
+
+def main():
+    out_path, N, scen, be = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    dist.init_process_group("gloo")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    g = workload.make_grouped_batch(scen, N, seed=4242)
+    G = g["group_size"]
+    inputs = {k: torch.from_numpy(np.ascontiguousarray(g[k])) for k in ("x0", "u_lin", "x_ref")}
+    solver = capi.Solver(capi.default_config(N, device=0, backend=be))
+
+    def solve_fn(sh):
+        B = sh["x0"].shape[0]
+        x0, ul, xr = (sh[k].to(dev) for k in ("x0", "u_lin", "x_ref"))
+        gid = (torch.arange(B, dtype=torch.int32) // G).to(dev)
+        uo = torch.empty((B, N, 2), dtype=torch.float32, device=dev)
+        xo = torch.empty((B, N + 1, 3), dtype=torch.float32, device=dev)
+        st = torch.empty(B, dtype=torch.int32, device=dev)
+        solver.solve_grouped_dev(x0, ul, xr, None, gid, max(1, -(-B // G)), uo, xo, st, None)
+        torch.cuda.synchronize(dev)
+        return {"u": uo.cpu(), "x": xo.cpu(), "status": st.cpu()}
+
+    out = solve_sharded(solve_fn, inputs, group_align=G)
+    if dist.get_rank() == 0:
+        np.savez(out_path, u=out["u"].numpy(), x=out["x"].numpy(), status=out["status"].numpy(),
+                 world=dist.get_world_size())
+    solver.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -613,3 +613,21 @@ def test_closed_loop_stream_warm(oracle, capi, be):
     warm.close()
     cold.close()
     assert np.mean(itw[1:]) <= np.mean(itc[1:]) + 1e-9, (np.mean(itw[1:]), np.mean(itc[1:]))
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2", "4"])
+@pytest.mark.parametrize("N", [30, 32])
+def test_lane_backend_reference_horizon_scratch(oracle, capi, monkeypatch, mode, N):
+    """The reference default horizon (params.yaml:12, N = 30) and N = 32 at a C5-sized batch on
+    every lane scratch placement (auto, LDS fp64, LDS fp32, HBM fp32): the auto policy's LDS
+    budget near its cap stays exact. Checked on a sample against the exact optimum."""
+    monkeypatch.setenv("F110QP_LANE_MODE", mode)
+    B = 4096
+    w = workload.make_batch(B, N, seed=3030 + N, heading="true", lateral=1.0, steer_range=0.6)
+    s = capi.Solver(capi.default_config(N, backend=capi.BACKEND_LANE))
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    assert (st == capi.SOLVED).all()
+    idx = np.arange(0, B, 7)
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
+    assert rel_err(u[idx], ur).max() <= 2e-6 and rel_err(x[idx], xr).max() <= 2e-6

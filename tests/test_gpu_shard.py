@@ -1,0 +1,55 @@
+"""Multi-process HIP evidence for the C4 split: two ranks (torch.distributed,
+gloo, both on GPU 0 of the box) each solve their scenario-aligned shard of a grouped C4-style
+batch through the C ABI; the all-gathered result is bit-identical to one process solving the
+whole batch (the QPs are independent: no data-path collective, the split changes nothing)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("N,scen,be", [(40, 9, "lane"), (20, 5, "wave")])
+def test_two_rank_hip_shards_bit_equal(capi, cuda, tmp_path, N, scen, be):
+    import torch
+
+    from f110qp import workload
+
+    backend = {"lane": capi.BACKEND_LANE, "wave": capi.BACKEND_WAVE}[be]
+    out = tmp_path / "sharded.npz"
+    env = {**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                    os.path.join(ROOT, "tests", "shard_gpu_worker.py"), str(out), str(N), str(scen), str(backend)],
+                   check=True, timeout=180, env=env, cwd=ROOT)
+    d = np.load(out)
+    assert int(d["world"]) == 2
+    g = workload.make_grouped_batch(scen, N, seed=4242)
+    B = g["x0"].shape[0]
+    s = capi.Solver(capi.default_config(N, device=0, backend=backend))
+    dev = torch.device("cuda", 0)
+    x0, ul, xr = (torch.from_numpy(np.ascontiguousarray(g[k])).to(dev) for k in ("x0", "u_lin", "x_ref"))
+    gid = (torch.arange(B, dtype=torch.int32) // g["group_size"]).to(dev)
+    uo = torch.empty((B, N, 2), dtype=torch.float32, device=dev)
+    xo = torch.empty((B, N + 1, 3), dtype=torch.float32, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    s.solve_grouped_dev(x0, ul, xr, None, gid, scen, uo, xo, st, None)
+    torch.cuda.synchronize()
+    s.close()
+    assert (st.cpu().numpy() == capi.SOLVED).all()
+    np.testing.assert_array_equal(d["status"], st.cpu().numpy())
+    np.testing.assert_array_equal(d["u"], uo.cpu().numpy())
+    np.testing.assert_array_equal(d["x"], xo.cpu().numpy())

@@ -1,0 +1,7 @@
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/c3b_tests.log 2>&1 || { grep -E "FAILED|Error|assert" gpurun_out/c3b_tests.log | head -20; exit 3; }
+tail -1 gpurun_out/c3b_tests.log
+for c in c3 c2; do
+timeout -k 10 200 python bench.py --no-cpu --no-latency --config $c --steps 20 > gpurun_out/c3b_$c.json 2>/dev/null || exit 9
+python -c "import json;d=json.load(open('gpurun_out/c3b_$c.json'));c=d['config'];print('$c', '%.3e'%d['value'], '%.1f'%(d['ms_per_step']*1e3), 'k %.1f'%(d['roofline']['kernel_ms_per_launch']*1e3), c['mean_active_set_iters'], c['max_active_set_iters'])"
+done
