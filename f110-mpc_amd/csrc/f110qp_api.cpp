@@ -447,6 +447,29 @@ int f110qp_condense_debug_dev(f110qp_ctx* c, int batch, const float* x0, const f
   return F110QP_OK;
 }
 
+int f110qp_qp_dims(int N, int* n, int* m, int* nnz_P, int* nnz_A) {
+  if (N < 1 || N > F110QP_MAX_HORIZON) return fail(F110QP_ERR_INVALID, "horizon must be in [1, 48]");
+  if (n) *n = 5 * N + 3;              // 3(N+1) states + 2N inputs (mpc.cpp:26-28)
+  if (m) *m = 7 * N + 5;              // dynamics + gap + input rows (mpc.cpp:29)
+  if (nnz_P) *nnz_P = 9 * (N + 1) + 4 * N;
+  if (nnz_A) *nnz_A = 26 * N + 9;
+  return F110QP_OK;
+}
+
+int f110qp_assemble_debug_dev(f110qp_ctx* c, const float* x0, const float* ul, const float* xr,
+                              const float* hs, int* Pc, int* Pr, double* Pv, double* q, int* Ac,
+                              int* Ar, double* Av, double* l, double* u, void* stream) {
+  if (!c) return fail(F110QP_ERR_INVALID, "ctx is NULL");
+  if (!x0 || !ul || !xr || !Pc || !Pr || !Pv || !q || !Ac || !Ar || !Av || !l || !u)
+    return fail(F110QP_ERR_INVALID, "NULL pointer argument");
+  const int gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
+  if (gap && !hs) return fail(F110QP_ERR_INVALID, "gap_mode ACTIVE needs the halfspace array");
+  hipError_t e = f110qp::launch_assemble(c->kp, x0, ul, xr, hs, gap, Pc, Pr, Pv, q, Ac, Ar, Av, l, u,
+                                         (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "assemble kernel launch");
+  return F110QP_OK;
+}
+
 // Constraints::FindHalfSpaces (src/constraints.cpp:116-265) for one scan, host code with the
 // reference's float32 member types; the ROS marker publish (:191-229) is not reproduced.
 int f110qp_find_half_spaces(const double state[3], const float* ranges, int nr, float angle_min,

@@ -83,6 +83,11 @@ hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const 
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* u_lin,
                                  const float* x_ref, double* H, double* g, hipStream_t stream);
 
+// One instance's (P, q, A, l, u) in the reference's CSC layout (assemble_kernel.hip).
+hipError_t launch_assemble(const KParams& P, const float* x0, const float* u_lin, const float* x_ref,
+                           const float* hs, int gap_active, int* Pc, int* Pr, double* Pv, double* q,
+                           int* Ac, int* Ar, double* Av, double* l, double* u, hipStream_t stream);
+
 // Planning stage (plan_kernels.hip): grid size, candidate count / length, float params.
 struct PlanKParams {
   int G;            // grid_blocks_ = size_ / discrete_

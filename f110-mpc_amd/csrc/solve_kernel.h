@@ -35,6 +35,8 @@
 
 #include "f110qp_kernels.h"
 
+#include "linearize.h"
+
 namespace f110qp {
 
 // Diagnostic build only (-DF110QP_STAMPS): per-phase s_memtime deltas of every wave, read back
@@ -200,34 +202,6 @@ __device__ __forceinline__ void wave_argmin(float& val, int& idx) {
   amin_step(v0, i0, readlane_f(val, 48), readlane_i(idx, 48));
   val = v0;
   idx = i0;
-}
-
-// ------------------------------------------------------------------------------------------
-// linearised model, fp64 (model.cpp:30-59; L = 0.3302f at :32; dt is the float MPC::dt_)
-// ------------------------------------------------------------------------------------------
-struct Lin {
-  double th0, a02, a12, b00, b10, b20, b21, c0, c1, c2;
-};
-
-__device__ __forceinline__ Lin linearize(double th, double v, double d, float dtf) {
-  const double dt = (double)dtf;
-  const double L = (double)0.3302f;
-  double sn, cs, sd, cd;
-  sincos(th, &sn, &cs);
-  sincos(d, &sd, &cd);
-  const double sec2 = 1.0 / (cd * cd);  // pow(cos(d), -2)
-  Lin M;
-  M.th0 = th;
-  M.a02 = -1 * v * sn * dt;           // :42
-  M.a12 = v * cs * dt;                // :43
-  M.b00 = cs * dt;                    // :48
-  M.b10 = sn * dt;                    // :49
-  M.b20 = (sd / cd) * dt / L;         // :50 tan(d)
-  M.b21 = v * sec2 * dt / L;          // :51
-  M.c0 = v * th * sn * dt;            // :53
-  M.c1 = -1 * v * th * cs * dt;       // :54
-  M.c2 = -1 * d * v * sec2 * dt / L;  // :55
-  return M;
 }
 
 // Forward rollout of u (one value per variable) in fp64. Returns, for each row, the

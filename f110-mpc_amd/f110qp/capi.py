@@ -55,6 +55,8 @@ EXPORTED = (
     "f110qp_solve_grouped",
     "f110qp_solve_grouped_dev",
     "f110qp_condense_debug_dev",
+    "f110qp_qp_dims",
+    "f110qp_assemble_debug_dev",
     "f110qp_warm_reset",
     "f110qp_find_half_spaces",
     "f110qp_find_half_spaces_dev",
@@ -125,6 +127,8 @@ def load():
     L.f110qp_solve_grouped_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 5
     L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
     L.f110qp_warm_reset.argtypes = [C.c_void_p]
+    L.f110qp_qp_dims.argtypes = [C.c_int] + [C.POINTER(C.c_int)] * 4
+    L.f110qp_assemble_debug_dev.argtypes = [C.c_void_p] + [fp] * 14
     L.f110qp_find_half_spaces.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_float), C.c_int,
                                           C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
                                           C.c_float, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -159,6 +163,13 @@ def default_config(horizon: int, **over) -> Config:
         else:
             setattr(c, k, v)
     return c
+
+
+def qp_dims(horizon: int):
+    """(n, m, nnz_P, nnz_A) of the reference's OSQP problem (f110qp_qp_dims)."""
+    v = [C.c_int() for _ in range(4)]
+    _check(load().f110qp_qp_dims(horizon, *[C.byref(x) for x in v]), "f110qp_qp_dims")
+    return tuple(x.value for x in v)
 
 
 def _p(a):
@@ -259,6 +270,35 @@ class Solver:
             if rc != OK:
                 _check(rc, "f110qp_solve_grouped_dev")
         return launch
+
+    def assemble_debug(self, x0, u_lin, x_ref, halfspace=None):
+        """f110qp_assemble_debug_dev for one instance (host arrays in; the device computes; host
+        dict of the CSC arrays out, the oracle.assemble layout)."""
+        import torch
+
+        N = self.horizon
+        n, m, nzp, nza = qp_dims(N)
+        dev = torch.device("cuda", self.config.device)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32).reshape(-1)).to(dev)  # noqa: E731
+        x0d, uld, xrd = t(x0), t(u_lin), t(x_ref)
+        hsd = None if halfspace is None else t(halfspace)
+        out = {"P_colptr": torch.empty(n + 1, dtype=torch.int32, device=dev),
+               "P_rowind": torch.empty(nzp, dtype=torch.int32, device=dev),
+               "P_val": torch.empty(nzp, dtype=torch.float64, device=dev),
+               "q": torch.empty(n, dtype=torch.float64, device=dev),
+               "A_colptr": torch.empty(n + 1, dtype=torch.int32, device=dev),
+               "A_rowind": torch.empty(nza, dtype=torch.int32, device=dev),
+               "A_val": torch.empty(nza, dtype=torch.float64, device=dev),
+               "l": torch.empty(m, dtype=torch.float64, device=dev),
+               "u": torch.empty(m, dtype=torch.float64, device=dev)}
+        stream = torch.cuda.current_stream(dev)
+        o = out
+        _check(self.lib.f110qp_assemble_debug_dev(self._h, _tp(x0d), _tp(uld), _tp(xrd), _tp(hsd), _tp(o["P_colptr"]),
+                                                  _tp(o["P_rowind"]), _tp(o["P_val"]), _tp(o["q"]), _tp(o["A_colptr"]),
+                                                  _tp(o["A_rowind"]), _tp(o["A_val"]), _tp(o["l"]), _tp(o["u"]),
+                                                  C.c_void_p(stream.cuda_stream)), "f110qp_assemble_debug_dev")
+        torch.cuda.synchronize(dev)
+        return {k: v.cpu().numpy() for k, v in out.items()}
 
     def solve_grouped(self, x0, u_lin, x_ref, group, num_groups=None, halfspace=None):
         """Grouped solve on host arrays (f110qp_solve_grouped): group [B] int scenario ids."""

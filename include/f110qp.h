@@ -163,6 +163,23 @@ int f110qp_warm_reset(f110qp_ctx* ctx);
 int f110qp_condense_debug_dev(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
                               const float* x_ref, double* H_out, double* g_out, void* stream);
 
+/* Sizes of the reference's OSQP problem for horizon N (src/mpc.cpp:26-29): n = 5N+3 variables,
+ * m = 7N+5 constraints, and the stored nonzeros of P (9(N+1) + 4N) and A (26N + 9), explicit
+ * zeros of the dense blocks included. Returns F110QP_OK or F110QP_ERR_INVALID. */
+int f110qp_qp_dims(int horizon, int* n, int* m, int* nnz_P, int* nnz_A);
+
+/* Assembly-parity hook: ONE instance's QP exactly as
+ * MPC::Update leaves it for OsqpEigen (src/mpc.cpp:77-80, layouts :208-306), computed on the
+ * device from x0[3], u_lin[2], x_ref[S][3] (S = x_ref_points) and halfspace[6] (NULL: zeros) with
+ * the solve kernels' Model::Linearize: P (CSC: colptr[n+1], rowind/val[nnz_P]), q[n], A (CSC:
+ * colptr[n+1], rowind/val[nnz_A]), l[m], u[m]; +-1e30 = OsqpEigen::INFTY. gap_mode INACTIVE gives
+ * the shipped rows (stage-0 all-ones placeholder block, +-INFTY bounds), ACTIVE the C3 semantic.
+ * Device pointers, async on stream. */
+int f110qp_assemble_debug_dev(f110qp_ctx* ctx, const float* x0, const float* u_lin,
+                              const float* x_ref, const float* halfspace, int* P_colptr,
+                              int* P_rowind, double* P_val, double* q, int* A_colptr, int* A_rowind,
+                              double* A_val, double* l, double* u, void* stream);
+
 /* Constraints::FindHalfSpaces (src/constraints.cpp:116-265) for one scan, host code.
  * state[3] = (x, y, ori); writes l1[3], l2[3] = (a, b, c+0.5). Returns F110QP_OK, or
  * F110QP_ERR_INVALID when the scan holds no gap (the reference then reads ranges[-1]). */

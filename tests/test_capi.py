@@ -126,3 +126,10 @@ def test_auto_backend_grouped_policy(capi):
     assert capi.auto_backend(40, 65536, False, grouped=True) == capi.BACKEND_LANE
     assert capi.auto_backend(40, 1024, False, grouped=True) == capi.BACKEND_WAVE
     assert capi.auto_backend(20, 4095, False, grouped=True) == capi.BACKEND_WAVE
+
+
+def test_qp_dims_match_reference_sizes(capi, oracle):
+    """f110qp_qp_dims: the reference's n = 5N+3, m = 7N+5 (src/mpc.cpp:26-29) and the stored
+    nonzeros of P and A, equal to the oracle's assembly for every horizon."""
+    for N in (1, 20, 30, 40, 48):
+        assert capi.qp_dims(N) == oracle.dims(N)

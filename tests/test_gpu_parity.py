@@ -631,3 +631,33 @@ def test_lane_backend_reference_horizon_scratch(oracle, capi, monkeypatch, mode,
     idx = np.arange(0, B, 7)
     ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
     assert rel_err(u[idx], ur).max() <= 2e-6 and rel_err(x[idx], xr).max() <= 2e-6
+
+
+@pytest.mark.parametrize("gap", [False, True])
+@pytest.mark.parametrize("N", [1, 20, 40])
+def test_assembly_hook_matches_reference_layout(oracle, capi, N, gap):
+    """f110qp_assemble_debug_dev: the product's reading of the reference QP on the
+    device equals the oracle's restatement of src/mpc.cpp:208-306 entry by entry: identical CSC
+    structure (explicit zeros, the stage-0 all-ones gap block of the shipped code, the C3 rows),
+    identical bounds, q with the terminal x_ref[N-1]; values to fp64 rounding (device vs host libm
+    sin/cos in Linearize, 1 ulp)."""
+    w = workload.make_batch(8, N, seed=600 + N, heading="true")
+    hs_all = None
+    if gap:
+        ranges, *geom = workload.make_scans(8, seed=600 + N)
+        hs_all = halfspaces_oracle(oracle, w["x0"], ranges, geom)
+    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE))
+    prm = oracle.params(N)
+    for b in range(8):
+        h = None if hs_all is None else hs_all[b]
+        got = s.assemble_debug(w["x0"][b], w["u_lin"][b], w["x_ref"][b], h)
+        ref = oracle.assemble(prm, w["x0"][b].astype(np.float64), w["u_lin"][b].astype(np.float64),
+                              w["x_ref"][b].astype(np.float64), None if h is None else h.astype(np.float64), gap)
+        for k in ("P_colptr", "P_rowind", "A_colptr", "A_rowind"):
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+        for k in ("P_val", "q"):
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+        for k in ("A_val", "l", "u"):  # A, B, C entries carry the device/host sin/cos ulp
+            np.testing.assert_allclose(got[k], ref[k], rtol=1e-15, atol=1e-18, err_msg=k)
+        assert (got["A_val"] == 0).sum() == (ref["A_val"] == 0).sum()  # explicit zeros kept
+    s.close()
