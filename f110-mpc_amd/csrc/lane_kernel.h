@@ -47,6 +47,11 @@
 // input-minor order: the least-index single principal pivoting of Murty / Bard, finite for
 // box-constrained QPs with a positive definite Hessian, Judice & Pires 1989), so every QP is
 // solved inside this one launch; P.max_iter passes bound it (status MAX_ITER, NaN outputs).
+//
+// This header holds the kernel template; lane_inst.hip instantiates it per QPs-per-wave value
+// LQ (a compile-time stride: every LDS / scratch offset is an immediate, which removed ~45
+// address instructions per stage and pass), lane_launch.hip picks the instantiation.
+#pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -58,7 +63,7 @@ namespace f110qp {
 // f110qp_read_lane_stamps(). The shipped library never executes a stamp.
 #ifdef F110QP_STAMPS
 constexpr int kLaneStampSlots = 8;
-__device__ unsigned long long g_lstamps[4096 * kLaneStampSlots];
+__device__ unsigned long long g_lstamps[4096 * kLaneStampSlots];  // one TU per stamps build
 #define LSTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #define LACC(acc, since) acc += __builtin_amdgcn_s_memtime() - (since)
 #else
@@ -73,8 +78,8 @@ constexpr int ring_depth() { return SLDS ? 2 : 4; }
 
 
 // Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
-template <typename ST, bool SLDS>
-__global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B, const int L,
+template <typename ST, bool SLDS, int L>
+__global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                                                   const float* __restrict__ x0g,
                                                   const float* __restrict__ ulg,
                                                   const float* __restrict__ xrg,
@@ -363,8 +368,11 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B, 
                 const int ca = (old >> (2 * a)) & 3;
                 const double u = a ? u1 : u0, g = a ? g1 : g0;
                 const double lb = a ? lb1 : lb0, ub = a ? ub1 : ub0;
-                const bool nlo = ((ca == 1) ? g : 0.0) + (lb - u) > 0.0;
-                const bool nhi = !nlo && (((ca == 2) ? -g : 0.0) + (u - ub) > 0.0);
+                // a fixed input sits exactly on its bound (k carries the bound, its K row is
+                // zero), so the HIK test reduces to the multiplier's sign for a fixed input and
+                // to the bound test for a free one
+                const bool nlo = (ca == 1) ? (g > 0.0) : (ca == 0 && u < lb);
+                const bool nhi = !nlo && ((ca == 2) ? (g < 0.0) : (ca == 0 && u > ub));
                 const int nca = nlo ? 1 : (nhi ? 2 : 0);
                 if (nca != ca && !(single && flipped)) {
                   st = (st & ~(3 << (2 * a))) | (nca << (2 * a));
@@ -474,66 +482,24 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B, 
 #endif
 }
 
-template <typename ST, bool SLDS>
-static hipError_t launch_lane_t(const KParams& P, int B, int L, const float* x0, const float* ul,
-                                const float* xr, float* uo, float* xo, int* st, int* its,
-                                const WarmState& ws, const LaneWork& lw, size_t lds,
-                                hipStream_t s) {
+template <typename ST, bool SLDS, int L>
+hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
+                         float* uo, float* xo, int* st, int* its, const WarmState& ws,
+                         const LaneWork& lw, size_t lds, hipStream_t s) {
   const int waves = (B + L - 1) / L;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_kernel<ST, SLDS>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_kernel<ST, SLDS, L>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((lane_kernel<ST, SLDS>), dim3(waves), dim3(64), lds, s, P, B, L, x0, ul, xr,
+  hipLaunchKernelGGL((lane_kernel<ST, SLDS, L>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr,
                      uo, xo, st, its, lw.scratch, ws, lw.kmax);
   return hipGetLastError();
 }
 
-// QPs per wave: the smallest power of two (<= 64) that fits the batch in kLaneTargetWaves waves
-// (one per CU).
-int lane_qps_per_wave(int B, int qpw) {
-  if (qpw >= 1 && qpw <= 64 && (qpw & (qpw - 1)) == 0) return qpw;
-  int L = 1;
-  while (L < 64 && (B + L - 1) / L > kLaneTargetWaves) L <<= 1;
-  return L;
-}
-
-// LDS per wave: the staged references (12 N L B) + PDAS state (4 N L B) + Riccati scratch
-// (8 N L sizeof(ST)) (lane_mode 0 = auto; 1/2/3/4 force LDS fp64 / LDS fp32 / HBM fp64 / HBM
-// fp32).
-hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* ul,
-                       const float* xr, float* uo, float* xo, int* st, int* its,
-                       const WarmState& ws, const LaneWork& lw, hipStream_t s) {
-  if (B <= 0) return hipSuccess;
-  const int L = lane_qps_per_wave(B, lw.qpw);
-  const size_t N = (size_t)P.N;
-  const size_t base = N * L * (12 + 4);  // references + PDAS state
-  const size_t lds64 = base + N * 8 * L * sizeof(double), lds32 = base + N * 8 * L * sizeof(float);
-  const size_t cap = 160 * 1024;
-  int mode = lw.mode;
-  // auto: the scratch in LDS when every wave of the grid is resident with it (waves per CU x
-  // its LDS within the CU's 160 KiB): fp64 if that fits, else fp32; otherwise fp32 in the HBM
-  // workspace (the waves then stay resident on the 16 N L bytes of references + state alone).
-  // With the state recentred on x0 the fp32 gains and trajectories stay within ~1e-7 of the
-  // exact optimum (tests/test_gpu_parity.py::test_lane_backend_scratch_modes).
-  if (mode == 0) {
-    const size_t waves = ((size_t)B + L - 1) / L;
-    const size_t per_cu = (waves + 255) / 256;
-    mode = per_cu * lds64 <= cap ? 1 : per_cu * lds32 <= cap ? 2 : 4;
-  }
-  if (mode == 1 && lds64 <= cap)
-    return launch_lane_t<double, true>(P, B, L, x0, ul, xr, uo, xo, st, its, ws, lw, lds64, s);
-  if (mode == 2 && lds32 <= cap)
-    return launch_lane_t<float, true>(P, B, L, x0, ul, xr, uo, xo, st, its, ws, lw, lds32, s);
-  if (mode == 4 || mode == 2)
-    return launch_lane_t<float, false>(P, B, L, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
-  return launch_lane_t<double, false>(P, B, L, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
-}
-
 }  // namespace f110qp
 
-#ifdef F110QP_STAMPS
+#if defined(F110QP_STAMPS) && defined(F110QP_LANE_ALL)
 extern "C" int f110qp_read_lane_stamps(unsigned long long* host, int n) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(f110qp::g_lstamps),
                                   (size_t)n * f110qp::kLaneStampSlots * sizeof(unsigned long long));

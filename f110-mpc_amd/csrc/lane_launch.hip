@@ -1,0 +1,76 @@
+// lane_launch.hip — the lane back end's launch policy: QPs per wave L and the scratch placement,
+// dispatched to the per-L instantiations of lane_kernel.h (lane_inst.hip). With F110QP_LANE_ALL
+// (the -DF110QP_STAMPS diagnostic build) this one file instantiates every variant itself.
+#ifdef F110QP_LANE_ALL
+#include "lane_kernel.h"
+#else
+#include <hip/hip_runtime.h>
+
+#include "f110qp_kernels.h"
+#endif
+
+namespace f110qp {
+
+#ifndef F110QP_LANE_ALL
+template <typename ST, bool SLDS, int L>
+hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
+                         float* uo, float* xo, int* st, int* its, const WarmState& ws,
+                         const LaneWork& lw, size_t lds, hipStream_t s);  // lane_inst.hip
+#endif
+
+// QPs per wave: the smallest power of two (<= 64) that fits the batch in kLaneTargetWaves waves
+// (one per CU).
+int lane_qps_per_wave(int B, int qpw) {
+  if (qpw >= 1 && qpw <= 64 && (qpw & (qpw - 1)) == 0) return qpw;
+  int L = 1;
+  while (L < 64 && (B + L - 1) / L > kLaneTargetWaves) L <<= 1;
+  return L;
+}
+
+template <int L>
+static hipError_t launch_lq(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
+                            float* uo, float* xo, int* st, int* its, const WarmState& ws,
+                            const LaneWork& lw, hipStream_t s) {
+  const size_t N = (size_t)P.N;
+  const size_t base = N * L * (12 + 4);  // references + PDAS state
+  const size_t lds64 = base + N * 8 * L * sizeof(double), lds32 = base + N * 8 * L * sizeof(float);
+  const size_t cap = 160 * 1024;
+  int mode = lw.mode;
+  // auto: the scratch in LDS when every wave of the grid is resident with it (waves per CU x
+  // its LDS within the CU's 160 KiB): fp64 if that fits, else fp32; otherwise fp32 in the HBM
+  // workspace (the waves then stay resident on the 16 N L bytes of references + state alone).
+  // With the state recentred on x0 the fp32 gains and trajectories stay within ~1e-7 of the
+  // exact optimum (tests/test_gpu_parity.py::test_lane_backend_scratch_modes).
+  if (mode == 0) {
+    const size_t waves = ((size_t)B + L - 1) / L;
+    const size_t per_cu = (waves + 255) / 256;
+    mode = per_cu * lds64 <= cap ? 1 : per_cu * lds32 <= cap ? 2 : 4;
+  }
+  if (mode == 1 && lds64 <= cap)
+    return launch_lane_t<double, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds64, s);
+  if (mode == 2 && lds32 <= cap)
+    return launch_lane_t<float, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds32, s);
+  if (mode == 4 || mode == 2)
+    return launch_lane_t<float, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
+  return launch_lane_t<double, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
+}
+
+// LDS per wave: the staged references (12 N L B) + PDAS state (4 N L B) + Riccati scratch
+// (8 N L sizeof(ST)) (lane_mode 0 = auto; 1/2/3/4 force LDS fp64 / LDS fp32 / HBM fp64 / HBM
+// fp32).
+hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* ul,
+                       const float* xr, float* uo, float* xo, int* st, int* its,
+                       const WarmState& ws, const LaneWork& lw, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  switch (lane_qps_per_wave(B, lw.qpw)) {
+    case 1: return launch_lq<1>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+    case 2: return launch_lq<2>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+    case 4: return launch_lq<4>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+    case 8: return launch_lq<8>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+    case 16: return launch_lq<16>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+    case 32: return launch_lq<32>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+    default: return launch_lq<64>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+  }
+}
+
+}  // namespace f110qp
