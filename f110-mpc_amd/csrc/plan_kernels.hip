@@ -64,7 +64,51 @@ __device__ __forceinline__ void world_to_occ(float disc, int G, float o0, float 
   row = cvtt((y - o1) / disc + (float)(G / 2));
 }
 
+// Trajectory::get_best_global_idx's distance test for waypoint i (trajectory.cpp:92-108): the
+// waypoint in the car frame (TransformPoint), -1 when it is behind the car (:100), else
+// |dist - lookahead|.
+__device__ __forceinline__ double waypoint_diff(const Basis& R, double tx, double ty,
+                                                const double* __restrict__ wp, int i,
+                                                float lookahead) {
+  const double wx = (double)(float)wp[2 * i], wy = (double)(float)wp[2 * i + 1];
+  const double rx = R.r00 * wx + R.r10 * wy + 0.0 * 0.0;
+  const double ry = R.r01 * wx + R.r11 * wy + 0.0 * 0.0;
+  const float cx = (float)(rx + tx), cy = (float)(ry + ty);
+  if (cx < 0) return -1.0;
+  const double dist = sqrt((double)cx * (double)cx + (double)cy * (double)cy);
+  return fabs(dist - (double)lookahead);
+}
+
+// (bits(FLT_MAX), ~0): the float-minimum's initial value (trajectory.cpp:88) with no index
+constexpr unsigned long long kWpNone = (0x7f7fffffull << 32) | 0xffffffffull;
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const unsigned long long o = __shfl_xor(v, m, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = max(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
 }  // namespace
+
+// Diagnostic build only (-DF110QP_STAMPS): per-workgroup cycles at each phase boundary (thread 0),
+// read back with f110qp_read_plan_stamps(). The shipped library never executes a stamp.
+#ifdef F110QP_STAMPS
+constexpr int kPlanStampSlots = 8;
+__device__ unsigned long long g_pstamps[4096 * kPlanStampSlots];
+#define PSTAMP(k) \
+  if (tid == 0 && b < 4096) g_pstamps[(size_t)b * kPlanStampSlots + (k)] = __builtin_amdgcn_s_memtime() - t_start
+#else
+#define PSTAMP(k)
+#endif
 
 __global__ __launch_bounds__(256) void plan_kernel(const PlanKParams K, const int B,
                                                    const double* __restrict__ pose,
@@ -84,12 +128,15 @@ __global__ __launch_bounds__(256) void plan_kernel(const PlanKParams K, const in
   extern __shared__ __attribute__((aligned(16))) unsigned char plds[];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
+#ifdef F110QP_STAMPS
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
   const int G = K.G, T = K.T, P = K.P;
   const int gwords = (G * G + 3) / 4;
-  unsigned long long* red64 = reinterpret_cast<unsigned long long*>(plds);  // DWA min (8 B)
-  unsigned* red = reinterpret_cast<unsigned*>(plds + 8);                   // 4 reductions
-  int* vflag = reinterpret_cast<int*>(plds + 24);                          // [T]
-  unsigned char* grid = plds + 24 + 4 * T;                                 // [G][G]
+  unsigned long long* red64 = reinterpret_cast<unsigned long long*>(plds);  // DWA min, wp key
+  unsigned* red = reinterpret_cast<unsigned*>(plds + 16);                  // 4 reductions
+  int* vflag = reinterpret_cast<int*>(plds + 32);                          // [T]
+  unsigned char* grid = plds + 32 + 4 * T;                                 // [G][G]
 
   const double px = pose[4 * b + 0], py = pose[4 * b + 1];
   const double qz = pose[4 * b + 2], qw = pose[4 * b + 3];
@@ -103,33 +150,81 @@ __global__ __launch_bounds__(256) void plan_kernel(const PlanKParams K, const in
   for (int w = tid; w < gwords; w += 256) reinterpret_cast<unsigned*>(grid)[w] = 0u;
   for (int i = tid; i < T; i += 256) vflag[i] = 1;
   if (tid == 0) {
-    red[0] = 0x7f7fffffu;  // FLT_MAX bits: float min of the waypoint distances
-    red[1] = 0x7fffffffu;  // first index reaching it
-    red[2] = 0u;           // 1 + last later index strictly below it
+    red[2] = 0u;           // 1 + last waypoint index strictly below the float minimum
     red64[0] = 0x7fefffffffffffffull;  // DBL_MAX bits: DWA min distance
+    red64[1] = kWpNone;    // (float minimum, first index reaching it)
   }
   __syncthreads();
+  PSTAMP(0);
   int num_scans = (int)((angle_max - angle_min) / angle_inc + 1);  // :66
   if (num_scans > nr) num_scans = nr;
   const float* rr = ranges + (size_t)b * nr;
+  // The dilation loops (:77-78) visit the same float offsets for every beam, and the column of
+  // WorldToOccupancy depends only on x, the row only on y: run the offset loop once, then per
+  // beam convert nd columns and nd rows (2 nd divisions instead of 2 nd^2) and mark their nd^2
+  // products. kDil offsets per axis cover dilation / discrete < 4 (the default has nd = 4).
+  constexpr int kDil = 8;
+  float offs[kDil];
+  int nd = 0;
+  bool more = true;
+  {
+    float o = -K.dilation;
+#pragma unroll
+    for (int k = 0; k < kDil; k++) {
+      more = more && (o <= K.dilation);
+      if (more) nd = k + 1;
+      offs[k] = o;
+      o += K.discrete;
+    }
+    more = more && (o <= K.dilation);  // the loop would run past kDil offsets
+  }
+  const float halfG = (float)(G / 2), fG = (float)G;
   for (int ii = tid; ii < num_scans; ii += 256) {
     const float angle = angle_min + ii * angle_inc + cur;                 // :71
-    float cx = (float)((double)rr[ii] * cos((double)angle));             // PolarToCartesian
-    float cy = (float)((double)rr[ii] * sin((double)angle));
+    double sa, ca;
+    sincos((double)angle, &sa, &ca);
+    const double rng = (double)rr[ii];
+    float cx = (float)(rng * ca);                                          // PolarToCartesian
+    float cy = (float)(rng * sa);
     cx += o0;
     cy += o1;
-    for (float xo = -K.dilation; xo <= K.dilation; xo += K.discrete)     // :77-78
-      for (float yo = -K.dilation; yo <= K.dilation; yo += K.discrete) {
-        int col, row;
-        world_to_occ(K.discrete, G, o0, o1, cx + xo, cy + yo, col, row);
-        if (col >= 0 && col < G && row >= 0 && row < G) grid[row * G + col] = 1;
+    if (!more) {
+      // cvtt(v) lands in [0, G) exactly when -1 < v < G (NaN fails both compares)
+      int col[kDil], row[kDil];
+      bool cok[kDil], rok[kDil];
+#pragma unroll
+      for (int k = 0; k < kDil; k++) {
+        const float vx = (cx + offs[k] - o0) / K.discrete + halfG;
+        const float vy = (cy + offs[k] - o1) / K.discrete + halfG;
+        cok[k] = k < nd && vx > -1.0f && vx < fG;
+        rok[k] = k < nd && vy > -1.0f && vy < fG;
+        col[k] = cok[k] ? (int)vx : 0;
+        row[k] = rok[k] ? (int)vy * G : 0;
       }
+#pragma unroll
+      for (int i = 0; i < kDil; i++)
+#pragma unroll
+        for (int j = 0; j < kDil; j++)
+          if (cok[i] && rok[j]) grid[row[j] + col[i]] = 1;
+    } else {
+      for (float xo = -K.dilation; xo <= K.dilation; xo += K.discrete)   // :77-78
+        for (float yo = -K.dilation; yo <= K.dilation; yo += K.discrete) {
+          int c, r;
+          world_to_occ(K.discrete, G, o0, o1, cx + xo, cy + yo, c, r);
+          if (c >= 0 && c < G && r >= 0 && r < G) grid[r * G + c] = 1;
+        }
+    }
   }
   __syncthreads();
+  PSTAMP(1);
 
   // ---- collision check of the candidate table (:76-113) -----------------------------------
+  // candidate of point k = k / P: (k + 0.5) * (1/P) is at least 0.5/P from an integer and its
+  // float error stays below 2^-5/P for k < T * P <= 2^18, so the truncation is exact
+  const float invP = 1.0f / (float)P;
   for (int k = tid; k < T * P; k += 256) {
-    const int i = k / P;
+    const int i = (int)(((float)k + 0.5f) * invP);
+    if (!vflag[i]) continue;  // an earlier point already hit
     const double* pt = table + (size_t)k * 3;
     float wx, wy;
     car_to_world(R, px, py, (float)pt[0], (float)pt[1], wx, wy);
@@ -139,57 +234,54 @@ __global__ __launch_bounds__(256) void plan_kernel(const PlanKParams K, const in
     if (!in || grid[row * G + col]) vflag[i] = 0;                        // :94-105
   }
   __syncthreads();
+  // nvalid > 0 is all the selection needs (:118-121)
+  bool anyv = false;
+  for (int i = tid; i < T; i += 256) anyv |= vflag[i] != 0;
+  const bool any_valid = __syncthreads_or(anyv);
+  PSTAMP(2);
 
   // ---- best waypoint (trajectory.cpp:81-126) -----------------------------------------------
   // The reference keeps the running minimum in a float: index i is taken when
-  // d_i < float(min so far). Equivalently: F = min_i float(d_i); i0 = first index with
-  // float(d_i) = F (it is always taken, and the minimum stays F afterwards); the result is the
-  // last j > i0 with d_j < F (double comparison), or i0.
+  // d_i < float(min so far). Equivalently: F = min_i float(d_i) over the waypoints ahead,
+  // i0 = the first index with float(d_i) = F (it is always taken, and the minimum stays F
+  // afterwards); the result is the last j with d_j < F (double comparison; such a j has
+  // float(d_j) = F, so j >= i0), or i0. Pass 1 reduces the key (bits(float d_i), i) to its
+  // minimum, which is (F, i0) at once; pass 2 reduces the last j. Each thread folds its own
+  // waypoints, the wave folds its lanes, and one LDS atomic per wave publishes the result.
   const double tx = R.r00 * (-px) + R.r10 * (-py) + 0.0 * (-0.0);  // inverse: basis^T, -basis^T p
   const double ty = R.r01 * (-px) + R.r11 * (-py) + 0.0 * (-0.0);
+  unsigned long long key = kWpNone;
   for (int i = tid; i < W; i += 256) {
-    const double wx = (double)(float)wp[2 * i], wy = (double)(float)wp[2 * i + 1];
-    const double rx = R.r00 * wx + R.r10 * wy + 0.0 * 0.0;
-    const double ry = R.r01 * wx + R.r11 * wy + 0.0 * 0.0;
-    const float cx = (float)(rx + tx), cy = (float)(ry + ty);            // TransformPoint
-    if (cx < 0) continue;                                                 // :100
-    const double dist = sqrt((double)cx * (double)cx + (double)cy * (double)cy);
-    const double diff = fabs(dist - (double)K.lookahead);
-    atomicMin(&red[0], __float_as_uint((float)diff));                     // diff >= 0
+    const double diff = waypoint_diff(R, tx, ty, wp, i, K.lookahead);
+    if (diff < 0.0) continue;                                             // behind the car (:100)
+    const float fd = (float)diff;
+    const unsigned long long k = ((unsigned long long)__float_as_uint(fd) << 32) | (unsigned)i;
+    key = k < key ? k : key;  // inf / NaN bits sort above kWpNone's FLT_MAX and never win
   }
+  key = wave_min_u64(key);
+  if ((tid & 63) == 0 && key < kWpNone) atomicMin(&red64[1], key);
   __syncthreads();
-  const float F = __uint_as_float(red[0]);
-  for (int i = tid; i < W; i += 256) {
-    const double wx = (double)(float)wp[2 * i], wy = (double)(float)wp[2 * i + 1];
-    const double rx = R.r00 * wx + R.r10 * wy + 0.0 * 0.0;
-    const double ry = R.r01 * wx + R.r11 * wy + 0.0 * 0.0;
-    const float cx = (float)(rx + tx), cy = (float)(ry + ty);
-    if (cx < 0) continue;
-    const double dist = sqrt((double)cx * (double)cx + (double)cy * (double)cy);
-    const double diff = fabs(dist - (double)K.lookahead);
-    if ((float)diff == F) atomicMin(&red[1], (unsigned)i);
+  PSTAMP(3);
+  const unsigned long long kmin = red64[1];
+  int closest = -1;
+  if (kmin < kWpNone) {  // uniform
+    const int i0 = (int)(unsigned)kmin;
+    const float F = __uint_as_float((unsigned)(kmin >> 32));
+    int jl = -1;
+    for (int i = tid; i < W; i += 256) {
+      const double diff = waypoint_diff(R, tx, ty, wp, i, K.lookahead);
+      if (diff >= 0.0 && diff < (double)F) jl = i;
+    }
+    jl = wave_max_i32(jl);
+    if ((tid & 63) == 0 && jl >= 0) atomicMax(&red[2], (unsigned)(jl + 1));
+    __syncthreads();
+    closest = max(i0, (int)red[2] - 1);
   }
-  __syncthreads();
-  const int i0 = (int)red[1];
-  for (int i = tid; i < W; i += 256) {
-    if (i <= i0) continue;
-    const double wx = (double)(float)wp[2 * i], wy = (double)(float)wp[2 * i + 1];
-    const double rx = R.r00 * wx + R.r10 * wy + 0.0 * 0.0;
-    const double ry = R.r01 * wx + R.r11 * wy + 0.0 * 0.0;
-    const float cx = (float)(rx + tx), cy = (float)(ry + ty);
-    if (cx < 0) continue;
-    const double dist = sqrt((double)cx * (double)cx + (double)cy * (double)cy);
-    const double diff = fabs(dist - (double)K.lookahead);
-    if (diff < (double)F) atomicMax(&red[2], (unsigned)(i + 1));
-  }
-  __syncthreads();
-  const int closest = (red[1] == 0x7fffffffu) ? -1 : (red[2] ? (int)red[2] - 1 : i0);
+  PSTAMP(4);
 
   // ---- end-point selection among the valid candidates (:122-145) ---------------------------
-  int nvalid = 0;
-  for (int i = 0; i < T; i++) nvalid += vflag[i];
   int best = -1;
-  if (nvalid > 0 && closest >= 0) {
+  if (any_valid && closest >= 0) {
     const double gx = (double)(float)wp[2 * closest], gy = (double)(float)wp[2 * closest + 1];
     for (int i = tid; i < T; i += 256) {
       if (!vflag[i]) continue;
@@ -213,14 +305,15 @@ __global__ __launch_bounds__(256) void plan_kernel(const PlanKParams K, const in
       if (sqrt(dx * dx + dy * dy) == dmin) atomicMin(&red[3], (unsigned)i);
     }
     __syncthreads();
-    best = (int)red[3];
+    best = red[3] == 0x7fffffffu ? -1 : (int)red[3];  // no finite distance: nothing to index
   }
 
+  PSTAMP(5);
   // ---- outputs: miniPath_ in the map frame (:145-152), x0, status ----------------------------
-  const int status = nvalid == 0 ? 1 : (closest < 0 ? 2 : 0);
+  const int status = !any_valid ? 1 : (closest < 0 ? 2 : 0);
   if (tid == 0) {
     status_out[b] = status;
-    best_global[b] = nvalid == 0 ? -1 : closest;
+    best_global[b] = !any_valid ? -1 : closest;
     best_traj[b] = best;
     x0_out[3 * b + 0] = (float)px;  // State(position.x, position.y, GetCarOrientation) (:162)
     x0_out[3 * b + 1] = (float)py;
@@ -242,6 +335,7 @@ __global__ __launch_bounds__(256) void plan_kernel(const PlanKParams K, const in
     unsigned char* go = grid_out + (size_t)b * G * G;
     for (int k = tid; k < G * G; k += 256) go[k] = grid[k];
   }
+  PSTAMP(6);
 }
 
 hipError_t launch_plan(const PlanKParams& K, int B, const double* pose, const float* ranges,
@@ -250,7 +344,7 @@ hipError_t launch_plan(const PlanKParams& K, int B, const double* pose, const fl
                        unsigned char* valid_out, int* best_global, int* best_traj, float* x_ref,
                        float* x0, int* status, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  const size_t lds = 24 + 4 * (size_t)K.T + 4 * (size_t)((K.G * K.G + 3) / 4);
+  const size_t lds = 32 + 4 * (size_t)K.T + 4 * (size_t)((K.G * K.G + 3) / 4);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&plan_kernel),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -263,3 +357,10 @@ hipError_t launch_plan(const PlanKParams& K, int B, const double* pose, const fl
 }
 
 }  // namespace f110qp
+
+#ifdef F110QP_STAMPS
+extern "C" int f110qp_read_plan_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(f110qp::g_pstamps),
+                                  (size_t)n * f110qp::kPlanStampSlots * sizeof(unsigned long long));
+}
+#endif

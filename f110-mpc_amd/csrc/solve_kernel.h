@@ -311,10 +311,9 @@ struct Smem {
   static constexpr int NST = NUM / 2 + 1;  // stages 0..N
   alignas(16) float W[NUM][NUM];   // W = H^-1, row-major (symmetric: row p == column p)
   float L[NUM][NUM + 1];           // Cholesky factor of S_A (lower), slots x slots
-  // gap rows only: V[slot][var] = W n_slot and S_A = N_A' W N_A. With box rows alone both are
+  // gap rows only: V[slot][var] = W n_slot. With box rows alone V and S_A = N_A' W N_A are
   // signed entries of W (n_j = +-e_var) and are read from W directly.
   float V[GAP ? NUM : 1][NUM];
-  float S[GAP ? NUM : 1][NUM + 1];
   float vec[VN];                   // broadcast scratch (one entry per variable)
   float vec2[VN];
   float stX[NST], stY[NST];        // per-stage linear rollout (stage 1..N)
@@ -401,22 +400,20 @@ __device__ __forceinline__ void tri_backward(Smem<NUM, GAP>& sm, int lane, int q
   }
 }
 
-// S_A[i][c] for slot row i (constraint id sid_i) and uniform slot c
+// S_A[i][c] for box slot row i (constraint id sid_i) and uniform slot c: signed entries of W
 template <int NUM, bool GAP>
 __device__ __forceinline__ float s_entry(Smem<NUM, GAP>& sm, int row, int sid_i, int sid_c, int c) {
-  if constexpr (GAP) {
-    return sm.S[row][c];
-  } else {
-    const int vi = sid_i / 3, vc = sid_c / 3;
-    return box_sign(sid_i) * box_sign(sid_c) * sm.W[vi][vc];
-  }
+  const int vi = sid_i / 3, vc = sid_c / 3;
+  return box_sign(sid_i) * box_sign(sid_c) * sm.W[vi][vc];
 }
 
-// L = chol(S_A) of the q active slots (left-looking, one lane per slot row, L in LDS).
-// Sets this lane's 1/L[j][j] for its slots j < q (other entries keep their value).
+// L = chol(S_A) of the q active box slots (left-looking, one lane per slot row, L in LDS): the
+// box PDAS hand-over. Sets this lane's 1/L[j][j] for its slots j < q (other entries keep their
+// value). GI itself only appends a row (step 2) or deletes one (chol_delete).
 template <int NUM, bool GAP, int R>
 __device__ __forceinline__ void chol_slots(Smem<NUM, GAP>& sm, int lane, int q,
                                            const int (&slot_id)[R], float (&rd)[R]) {
+  static_assert(!GAP, "gap-row slots are factored incrementally");
   for (int c = 0; c < q; c++) {
     const int sid_c = GAP ? 0 : rl_i<R>(slot_id, c);
     float s[R];
@@ -445,6 +442,72 @@ __device__ __forceinline__ void chol_slots(Smem<NUM, GAP>& sm, int lane, int q,
       if (row == c) rd[r] = 1.f / dcc;
     }
     wsync();
+  }
+}
+
+// Delete slot kd from S_A = L L' (q slots before the call; rd = this lane's 1/L[j][j]).
+// The rows below kd move up one; each of them then carries one entry right of its diagonal,
+// which q - 1 - kd Givens rotations on the column pairs (j, j + 1) remove: the updated factor in
+// O(q^2) work and q - 1 - kd short dependent steps (hypot -> readlane -> 4 FMAs), instead of the
+// O(q^3) refactorisation of S_A with its q dependent column steps. After the shift every lane
+// touches only its own row, so the rotation loop needs no barrier.
+template <int NUM, bool GAP, int R>
+__device__ __forceinline__ void chol_delete(Smem<NUM, GAP>& sm, int lane, int q, int kd,
+                                            float (&rd)[R]) {
+  constexpr int kChunk = 8;
+  for (int c0 = 0; c0 < q; c0 += kChunk) {  // row s <- row s + 1 (columns 0..s + 1)
+    float t[R][kChunk];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int row = 64 * r + lane;
+      const bool mv = row >= kd && row < q - 1;
+#pragma unroll
+      for (int cc = 0; cc < kChunk; cc++) {
+        const int c = c0 + cc;
+        t[r][cc] = (mv && c < q && c <= row + 1) ? sm.L[row + 1][c] : 0.f;
+      }
+    }
+    wsync();
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int row = 64 * r + lane;
+      const bool mv = row >= kd && row < q - 1;
+#pragma unroll
+      for (int cc = 0; cc < kChunk; cc++) {
+        const int c = c0 + cc;
+        if (mv && c < q && c <= row + 1) sm.L[row][c] = t[r][cc];
+      }
+    }
+    wsync();
+  }
+  float carry[R];  // this row's entry in column j (rotated so far)
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int row = 64 * r + lane;
+    carry[r] = (row >= kd && row < q - 1) ? sm.L[row < NUM ? row : NUM - 1][kd] : 0.f;
+  }
+  for (int j = kd; j < q - 1; j++) {
+    float y[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int row = 64 * r + lane;
+      y[r] = (row >= j && row < q - 1) ? sm.L[row][j + 1] : 0.f;
+    }
+    const float a = rl_f<R>(carry, j), b = rl_f<R>(y, j);
+    const float h = sqrtf(a * a + b * b);
+    const float cs = a / h, sn = b / h;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int row = 64 * r + lane;
+      if (row > j && row < q - 1) {
+        sm.L[row][j] = fmaf(cs, carry[r], sn * y[r]);
+        carry[r] = fmaf(cs, y[r], -sn * carry[r]);
+      }
+      if (row == j) {
+        sm.L[row][j] = h;
+        rd[r] = 1.f / h;
+      }
+    }
   }
 }
 
@@ -1416,13 +1479,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #pragma unroll
         for (int r = 0; r < R; r++) {
           const int s = 64 * r + lane;
-          if (GAP) {
-            if (vv[r] < NUM) sm.V[q][vv[r]] = w[r];
-            if (s < q) {
-              sm.S[q][s] = vj[r];
-              sm.S[s][q] = vj[r];
-            }
-          }
+          if (GAP && vv[r] < NUM) sm.V[q][vv[r]] = w[r];
           if (s < q) sm.L[q][s] = lv[r];
           if (s == q) {
             slot_id[r] = p;
@@ -1431,10 +1488,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           }
           if (vv[r] == pown) actf[r] |= (1 << pt);
         }
-        if (lane == 0) {
-          if (GAP) sm.S[q][q] = nw;
-          sm.L[q][q] = sqrtf(pivv);
-        }
+        if (lane == 0) sm.L[q][q] = sqrtf(pivv);
         q++;
         wsync();
         STAMP_ACC(acc_upd, t_f);
@@ -1468,28 +1522,15 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           if (s == q - 1) { slot_id[r] = -1; mult[r] = 0.f; }
         }
         if (GAP) {
-          // remove slot kd from V (rows) and S (row and column): every lane moves only its own
-          // columns (V, S rows) or its own rows (S columns), so there is no cross-lane hazard
+          // remove slot kd from V (rows): every lane moves only its own column
 #pragma unroll
-          for (int r = 0; r < R; r++) {
-            if (vv[r] < NUM) {
-              for (int j = kd; j < q - 1; j++) {
-                sm.V[j][vv[r]] = sm.V[j + 1][vv[r]];
-                sm.S[j][vv[r]] = sm.S[j + 1][vv[r]];
-              }
-            }
-          }
-          wsync();
-#pragma unroll
-          for (int r = 0; r < R; r++) {
-            const int s = 64 * r + lane;
-            if (s < q - 1)
-              for (int i2 = kd; i2 < q - 1; i2++) sm.S[s][i2] = sm.S[s][i2 + 1];
-          }
+          for (int r = 0; r < R; r++)
+            if (vv[r] < NUM)
+              for (int j = kd; j < q - 1; j++) sm.V[j][vv[r]] = sm.V[j + 1][vv[r]];
         }
+        chol_delete<NUM, GAP, R>(sm, lane, q, kd, rdiag);
         q--;
         wsync();
-        chol_slots<NUM, GAP, R>(sm, lane, q, slot_id, rdiag);
       }
     }
   }

@@ -39,3 +39,7 @@ for i, n in enumerate(names):
     print(f"{n:28s} mean {v.mean():9.0f}  max {v.max():9.0f}  share {v.mean() / tot.mean() * 100:5.1f}%")
 it_ = buf[:, 15].astype(float)
 print(f"per-iteration: gi cycles/iter {(buf[:, 4].astype(float).sum() / max(1, it_.sum())):.0f}")
+q = np.percentile(tot, [50, 90, 99, 100])
+imax = int(np.argmax(tot))
+print(f"total cycles p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f} (slowest QP: {int(it_[imax])} iterations, "
+      f"gi {buf[imax, 4]:.0f}, refine {buf[imax, 5]:.0f}); iteration histogram {np.bincount(it_.astype(int), minlength=8)[:64].tolist()}")
