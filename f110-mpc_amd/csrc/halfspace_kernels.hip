@@ -53,6 +53,8 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   const int b = blockIdx.x * kHsWaves + (threadIdx.x >> 6);
   if (b >= B) return;  // whole waves only
   const float* r = ranges + (size_t)b * nr;
+  // the pose is only needed by the tail: loaded now, its latency hides behind the scan
+  const float st0 = states[3 * b + 0], st1 = states[3 * b + 1], st2 = states[3 * b + 2];
   // num_scans = (angle_max - angle_min) / angle_increment + 1 in float, truncated (:118)
   int num_scans = (int)((angle_max - angle_min) / angle_inc + 1.0f);
   if (num_scans > nr) num_scans = nr;
@@ -63,8 +65,8 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   bool top_open = false;      // beam 64 k - 1 open (wave-uniform)
   int w0 = -1;                // first in-window beam (wave-uniform)
   bool w0_open = false;
+  float v[kHsBatch];  // the last batch of blocks stays in registers for the tail
   for (int k0 = 0; k0 < nblk; k0 += kHsBatch) {
-    float v[kHsBatch];
 #pragma unroll
     for (int j = 0; j < kHsBatch; j++) {  // unconditional loads (clamped index): no exec masking
       const int p = 64 * (k0 + j) + lane;
@@ -119,8 +121,8 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
       for (int j = 0; j < 6; j++) o[j] = nanv;
     return;
   }
-  const double poseX = (double)states[3 * b + 0], poseY = (double)states[3 * b + 1];
-  const float cur = states[3 * b + 2];
+  const double poseX = (double)st0, poseY = (double)st1;
+  const float cur = st2;
   const float ang1 = angle_min + (float)best_lo * angle_inc + cur;  // :179-180
   const float ang2 = angle_min + (float)best_hi * angle_inc + cur;
   // even lanes evaluate the first end point's cos/sin, odd lanes the second (::cos/::sin(double))
@@ -128,10 +130,27 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   sincos((double)((lane & 1) ? ang2 : ang1), &sl, &cl);
   const double s1 = __shfl(sl, 0), c1d = __shfl(cl, 0);
   const double s2 = __shfl(sl, 1), c2d = __shfl(cl, 1);
-  const float p1x = (float)((double)r[best_lo] * c1d + poseX);  // :181-185
-  const float p1y = (float)((double)r[best_lo] * s1 + poseY);
-  const float p2x = (float)((double)r[best_hi] * c2d + poseX);
-  const float p2y = (float)((double)r[best_hi] * s2 + poseY);
+  // ranges[best_lo], ranges[best_hi]: from the registers of the last batch when the scan fits
+  // one batch (1,536 beams), else re-read (L2)
+  float rlo, rhi;
+  if (nblk <= kHsBatch) {
+    const int klo = best_lo >> 6, khi = best_hi >> 6;
+    float vlo = 0.f, vhi = 0.f;
+#pragma unroll
+    for (int j = 0; j < kHsBatch; j++) {
+      vlo = (j == klo) ? v[j] : vlo;
+      vhi = (j == khi) ? v[j] : vhi;
+    }
+    rlo = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vlo), best_lo & 63));
+    rhi = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vhi), best_hi & 63));
+  } else {
+    rlo = r[best_lo];
+    rhi = r[best_hi];
+  }
+  const float p1x = (float)((double)rlo * c1d + poseX);  // :181-185
+  const float p1y = (float)((double)rlo * s1 + poseY);
+  const float p2x = (float)((double)rhi * c2d + poseX);
+  const float p2y = (float)((double)rhi * s2 + poseY);
   const float px = (float)poseX, py = (float)poseY;
   float a1 = py - p1y, b1 = p1x - px;  // :233-253
   float c1 = px * p1y - py * p1x;
