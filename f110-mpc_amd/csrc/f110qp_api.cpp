@@ -100,6 +100,7 @@ struct f110qp_ctx {
   int lane_kmax = 16;        // lane back end: PDAS passes before single (least-index) flips
   int lane_mode = 0;         // lane scratch placement (LaneWork::mode)
   int lane_qpw = 0;          // lane QPs per wave (LaneWork::qpw, 0 = auto)
+  int lane_rot = 1;          // lane heading-frame kernel when q0 == q1 (LaneWork::rot)
   hipStream_t stream = nullptr;
 };
 
@@ -183,6 +184,8 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     const int v = std::atoi(em);
     if (v >= 0 && v <= 4) c->lane_mode = v;
   }
+  // test hook: F110QP_LANE_ROT=0 forces the lane back end's general-frame kernel
+  if (const char* er = std::getenv("F110QP_LANE_ROT")) c->lane_rot = std::atoi(er) != 0;
   // test hook: F110QP_PDAS_MAX caps the wave kernel's box PDAS passes (0 = GI from scratch)
   k.pdas_max = 10;
   if (const char* ep = std::getenv("F110QP_PDAS_MAX")) {
@@ -266,6 +269,7 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   lw->kmax = c->lane_kmax;
   lw->mode = c->lane_mode;
   lw->qpw = c->lane_qpw;
+  lw->rot = c->lane_rot;
   return F110QP_OK;
 }
 

@@ -78,7 +78,7 @@ constexpr int ring_depth() { return SLDS ? 2 : 4; }
 
 
 // Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
-template <typename ST, bool SLDS, int L>
+template <typename ST, bool SLDS, int L, bool ROT>
 __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                                                   const float* __restrict__ x0g,
                                                   const float* __restrict__ ulg,
@@ -155,15 +155,22 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
   sincos(th0, &sn, &cs);
   sincos(d, &sd, &cd);
   const double sec2 = 1.0 / (cd * cd);
-  const double a02 = -1 * v * sn * dt, a12 = v * cs * dt;                  // :42-43
-  const double b00 = cs * dt, b10 = sn * dt;                               // :48-49
+  // ROT (q0 == q1, the shipped params.yaml:1-2): the (x, y) offsets are expressed in the frame
+  // of the heading th0, s = cs dx + sn dy, n = cs dy - sn dx. Q = diag(q0, q0, q2) is invariant
+  // under that rotation and A = I + E, B become A = I + (v dt) e_n e_th', B = [dt 0; 0 0; b20 b21]
+  // (the rotated model.cpp:42-51 with cs^2 + sn^2 = 1): four zero entries that drop ~20 fp64
+  // operations of the backward Riccati stage and ~6 of the forward one.
+  const double a02 = ROT ? 0.0 : -1 * v * sn * dt;                         // :42
+  const double a12 = ROT ? v * dt : v * cs * dt;                           // :43
+  const double b00 = ROT ? dt : cs * dt, b10 = ROT ? 0.0 : sn * dt;        // :48-49
   const double b20 = (sd / cd) * dt / Lw, b21 = v * sec2 * dt / Lw;        // :50-51
   const double c0r = v * th0 * sn * dt, c1r = -1 * v * th0 * cs * dt;     // :53-54
   const double c2 = -1 * d * v * sec2 * dt / Lw;                           // :55
   // The state is recentred on x0 = (X0, Y0, th0): translation invariance in (x, y) and, for the
   // heading, x_{i+1} = x_i + a02 th_i + ... + c0 = x_i + a02 (th_i - th0) + ... + (c0 + a02 th0).
   // c0 + a02 th0 is zero up to rounding (model.cpp:42,53); keeping it as computed stays exact.
-  const double c0 = c0r + a02 * th0, c1 = c1r + a12 * th0;
+  // (In the rotated frame both are exactly zero in exact arithmetic and dropped.)
+  const double c0 = ROT ? 0.0 : c0r + a02 * th0, c1 = ROT ? 0.0 : c1r + a12 * th0;
   const double q0 = P.q[0], q1 = P.q[1], q2 = P.q[2], r0 = P.r[0], r1 = P.r[1];
   const double ud0 = P.udes[0], ud1 = P.udes[1];
   const double lb0 = (double)P.umin[0], lb1 = (double)P.umin[1];
@@ -217,8 +224,15 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
     }
   }
   auto ref = [&](int i, double& rx, double& ry, double& rt) {
-    rx = (double)xr_s[(3 * i + 0) * L + slot] - X0;
-    ry = (double)xr_s[(3 * i + 1) * L + slot] - Y0;
+    const double dx = (double)xr_s[(3 * i + 0) * L + slot] - X0;
+    const double dy = (double)xr_s[(3 * i + 1) * L + slot] - Y0;
+    if constexpr (ROT) {
+      rx = cs * dx + sn * dy;
+      ry = cs * dy - sn * dx;
+    } else {
+      rx = dx;
+      ry = dy;
+    }
     rt = (double)xr_s[(3 * i + 2) * L + slot] - th0;
   };
 
@@ -259,28 +273,33 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         const double rxi = rx, ryi = ry, rti = rt;
         if (i > 0) ref(i - 1, rx, ry, rt);  // next stage's reference, loaded a stage ahead
         // Riccati step of stage i against V_{i+1}(x) = 1/2 x'Px + p'x
-        const double g0 = P00 * c0 + P01 * c1 + P02 * c2 + p0;  // P C + p
-        const double g1 = P01 * c0 + P11 * c1 + P12 * c2 + p1;
-        const double g2 = P02 * c0 + P12 * c1 + P22 * c2 + p2;
-        const double pb0 = P00 * b00 + P01 * b10 + P02 * b20;      // P B[:,0]
-        const double pb1 = P01 * b00 + P11 * b10 + P12 * b20;
-        const double pb2 = P02 * b00 + P12 * b10 + P22 * b20;
+        // (ROT: the terms of the zero entries a02, b10, c0, c1 are not formed at all)
+        const double g0 = ROT ? P02 * c2 + p0 : P00 * c0 + P01 * c1 + P02 * c2 + p0;  // P C + p
+        const double g1 = ROT ? P12 * c2 + p1 : P01 * c0 + P11 * c1 + P12 * c2 + p1;
+        const double g2 = ROT ? P22 * c2 + p2 : P02 * c0 + P12 * c1 + P22 * c2 + p2;
+        const double pb0 = ROT ? P00 * b00 + P02 * b20 : P00 * b00 + P01 * b10 + P02 * b20;  // P B[:,0]
+        const double pb1 = ROT ? P01 * b00 + P12 * b20 : P01 * b00 + P11 * b10 + P12 * b20;
+        const double pb2 = ROT ? P02 * b00 + P22 * b20 : P02 * b00 + P12 * b10 + P22 * b20;
         const double pc0 = P02 * b21, pc1 = P12 * b21, pc2 = P22 * b21;  // P B[:,1]
-        const double H00 = r0 + b00 * pb0 + b10 * pb1 + b20 * pb2;  // R + B'PB
+        const double H00 = ROT ? r0 + b00 * pb0 + b20 * pb2 : r0 + b00 * pb0 + b10 * pb1 + b20 * pb2;  // R + B'PB
         const double H01 = b21 * pb2;
         const double H11 = r1 + b21 * pc2;
         // Hux = B'PA: row a = ((PB_a)_0, (PB_a)_1, (PB_a)_2 + a02 (PB_a)_0 + a12 (PB_a)_1)
-        const double X00 = pb0, X01 = pb1, X02 = pb2 + a02 * pb0 + a12 * pb1;
-        const double X10 = pc0, X11 = pc1, X12 = pc2 + a02 * pc0 + a12 * pc1;
-        const double h0 = -r0 * ud0 + b00 * g0 + b10 * g1 + b20 * g2;  // -R ud + B'g
+        const double X00 = pb0, X01 = pb1;
+        const double X02 = ROT ? pb2 + a12 * pb1 : pb2 + a02 * pb0 + a12 * pb1;
+        const double X10 = pc0, X11 = pc1;
+        const double X12 = ROT ? pc2 + a12 * pc1 : pc2 + a02 * pc0 + a12 * pc1;
+        const double h0 = ROT ? -r0 * ud0 + b00 * g0 + b20 * g2
+                              : -r0 * ud0 + b00 * g0 + b10 * g1 + b20 * g2;  // -R ud + B'g
         const double h1 = -r1 * ud1 + b21 * g2;
         // Hxx = Q + A'PA, hx = -Q r + A'g
-        const double e0 = P02 + a02 * P00 + a12 * P01, e1 = P12 + a02 * P01 + a12 * P11;
-        const double e2 = P22 + a02 * P02 + a12 * P12;
+        const double e0 = ROT ? P02 + a12 * P01 : P02 + a02 * P00 + a12 * P01;
+        const double e1 = ROT ? P12 + a12 * P11 : P12 + a02 * P01 + a12 * P11;
+        const double e2 = ROT ? P22 + a12 * P12 : P22 + a02 * P02 + a12 * P12;
         const double Y00 = q0 + P00, Y01 = P01, Y11 = q1 + P11, Y02 = e0, Y12 = e1;
-        const double Y22 = q2 + e2 + a02 * e0 + a12 * e1;
+        const double Y22 = ROT ? q2 + e2 + a12 * e1 : q2 + e2 + a02 * e0 + a12 * e1;
         const double hx0 = -q0 * rxi + g0, hx1 = -q1 * ryi + g1;
-        const double hx2 = -q2 * rti + g2 + a02 * g0 + a12 * g1;
+        const double hx2 = ROT ? -q2 * rti + g2 + a12 * g1 : -q2 * rti + g2 + a02 * g0 + a12 * g1;
         // masked 2x2 solve over the free inputs of the stage (fixed ones sit on their bound)
         const int ca0 = sti & 3, ca1 = (sti >> 2) & 3;
         const bool f0 = ca0 == 0, f1 = ca1 == 0;
@@ -356,9 +375,10 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
               // lambda_{i+1} = (I - E')(lambda_i - Q(x_i - r_i))
               const double w0 = l0 - q0 * (x0 - rxi), w1 = l1 - q1 * (x1 - ryi);
               const double w2 = l2 - q2 * (x2 - rti);
-              l0 = w0; l1 = w1; l2 = w2 - a02 * w0 - a12 * w1;
+              l0 = w0; l1 = w1; l2 = ROT ? w2 - a12 * w1 : w2 - a02 * w0 - a12 * w1;
               // gradient of the objective in u_i: g = R(u - ud) + B' lambda_{i+1}
-              const double g0 = r0 * (u0 - ud0) + b00 * l0 + b10 * l1 + b20 * l2;
+              const double g0 = ROT ? r0 * (u0 - ud0) + b00 * l0 + b20 * l2
+                                    : r0 * (u0 - ud0) + b00 * l0 + b10 * l1 + b20 * l2;
               const double g1 = r1 * (u1 - ud1) + b21 * l2;
               // PDAS re-guess (Hintermueller-Ito-Kunisch, c = 1), both inputs of the stage:
               // the multiplier of an active lower bound is g, of an active upper bound -g
@@ -383,8 +403,8 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                 changed = true;
                 ap[i * L] = st;
               }
-              const double nx0 = x0 + a02 * x2 + b00 * u0 + c0;
-              const double nx1 = x1 + a12 * x2 + b10 * u0 + c1;
+              const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
+              const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;
               const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
               x0 = nx0; x1 = nx1; x2 = nx2;
             }
@@ -426,15 +446,16 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
             ur[t][0] = s[0];
             ur[t][1] = s[L];
           }
-          const double nx0 = x0 + a02 * x2 + b00 * u0 + c0;
-          const double nx1 = x1 + a12 * x2 + b10 * u0 + c1;
+          const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
+          const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;
           const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
           x0 = nx0; x1 = nx1; x2 = nx2;
           if (owner) {
             uo[2 * i] = solved ? (float)u0 : nanv;
             uo[2 * i + 1] = solved ? (float)u1 : nanv;
-            xo[3 * i + 3] = solved ? (float)(x0 + X0) : nanv;
-            xo[3 * i + 4] = solved ? (float)(x1 + Y0) : nanv;
+            const double ox = ROT ? cs * x0 - sn * x1 : x0, oy = ROT ? sn * x0 + cs * x1 : x1;
+            xo[3 * i + 3] = solved ? (float)(ox + X0) : nanv;
+            xo[3 * i + 4] = solved ? (float)(oy + Y0) : nanv;
             xo[3 * i + 5] = solved ? (float)(x2 + th0) : nanv;
           }
         }
@@ -482,17 +503,17 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
 #endif
 }
 
-template <typename ST, bool SLDS, int L>
+template <typename ST, bool SLDS, int L, bool ROT>
 hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                          float* uo, float* xo, int* st, int* its, const WarmState& ws,
                          const LaneWork& lw, size_t lds, hipStream_t s) {
   const int waves = (B + L - 1) / L;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_kernel<ST, SLDS, L>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_kernel<ST, SLDS, L, ROT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((lane_kernel<ST, SLDS, L>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr,
+  hipLaunchKernelGGL((lane_kernel<ST, SLDS, L, ROT>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr,
                      uo, xo, st, its, lw.scratch, ws, lw.kmax);
   return hipGetLastError();
 }

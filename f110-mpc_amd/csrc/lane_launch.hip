@@ -12,7 +12,7 @@
 namespace f110qp {
 
 #ifndef F110QP_LANE_ALL
-template <typename ST, bool SLDS, int L>
+template <typename ST, bool SLDS, int L, bool ROT>
 hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                          float* uo, float* xo, int* st, int* its, const WarmState& ws,
                          const LaneWork& lw, size_t lds, hipStream_t s);  // lane_inst.hip
@@ -25,6 +25,16 @@ int lane_qps_per_wave(int B, int qpw) {
   int L = 1;
   while (L < 64 && (B + L - 1) / L > kLaneTargetWaves) L <<= 1;
   return L;
+}
+
+// the heading-frame variant when Q's (x, y) weights are equal (lane_kernel.h, ROT)
+template <typename ST, bool SLDS, int L>
+static hipError_t launch_rot(const KParams& P, int B, const float* x0, const float* ul,
+                             const float* xr, float* uo, float* xo, int* st, int* its,
+                             const WarmState& ws, const LaneWork& lw, size_t lds, hipStream_t s) {
+  if (lw.rot && P.q[0] == P.q[1])
+    return launch_lane_t<ST, SLDS, L, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
+  return launch_lane_t<ST, SLDS, L, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
 }
 
 template <int L>
@@ -47,12 +57,12 @@ static hipError_t launch_lq(const KParams& P, int B, const float* x0, const floa
     mode = per_cu * lds64 <= cap ? 1 : per_cu * lds32 <= cap ? 2 : 4;
   }
   if (mode == 1 && lds64 <= cap)
-    return launch_lane_t<double, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds64, s);
+    return launch_rot<double, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds64, s);
   if (mode == 2 && lds32 <= cap)
-    return launch_lane_t<float, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds32, s);
+    return launch_rot<float, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds32, s);
   if (mode == 4 || mode == 2)
-    return launch_lane_t<float, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
-  return launch_lane_t<double, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
+    return launch_rot<float, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
+  return launch_rot<double, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
 }
 
 // LDS per wave: the staged references (12 N L B) + PDAS state (4 N L B) + Riccati scratch

@@ -455,6 +455,22 @@ def test_lane_backend_custom_weights_and_far_origin(oracle, capi, be):
     assert rel_err(u, ur).max() <= TOL and rel_err(x, xr).max() <= TOL
 
 
+@pytest.mark.parametrize("rot", ["0", "1"])
+@pytest.mark.parametrize("N", [20, 40])
+def test_lane_backend_heading_frame(oracle, capi, monkeypatch, rot, N):
+    """q0 == q1 (the shipped params.yaml) runs the lane kernel in the frame of the heading
+    theta0 (lane_kernel.h ROT: four zero model entries); F110QP_LANE_ROT=0 forces the general
+    frame. Both give the exact optimum, also 1 km from the origin with headings all round the
+    circle, and agree with each other."""
+    monkeypatch.setenv("F110QP_LANE_ROT", rot)
+    w = workload.make_batch(1500, N, seed=6060 + N, heading="true", lateral=1.5, steer_range=1.0)
+    w["x0"][:, 2] = np.random.default_rng(N).uniform(-np.pi, np.pi, 1500).astype(np.float32)
+    w["x0"][:, :2] += np.float32(1000.0)
+    w["x_ref"][:, :, :2] += np.float32(1000.0)
+    u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
+    assert (st == capi.SOLVED).all()
+
+
 @pytest.mark.parametrize("be", RICCATI)
 @pytest.mark.parametrize("kmax,N", [("0", 20), ("1", 20), ("2", 40), ("0", 40)])
 def test_lane_backend_single_flip_fallback(oracle, capi, monkeypatch, be, kmax, N):
