@@ -269,9 +269,10 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
       for (int i = N - 1; i >= 0; i--) {
         ST* s = sp + (size_t)i * 8 * L;
         const int sti = nst;
-        if (i > 0) nst = ap[(i - 1) * L];
+        const int inx = i > 0 ? i - 1 : 0;  // clamped: loads without a branch (no register copies)
+        nst = ap[inx * L];
         const double rxi = rx, ryi = ry, rti = rt;
-        if (i > 0) ref(i - 1, rx, ry, rt);  // next stage's reference, loaded a stage ahead
+        ref(inx, rx, ry, rt);  // next stage's reference, loaded a stage ahead
         // Riccati step of stage i against V_{i+1}(x) = 1/2 x'Px + p'x
         // (ROT: the terms of the zero entries a02, b10, c0, c1 are not formed at all)
         const double g0 = ROT ? P02 * c2 + p0 : P00 * c0 + P01 * c1 + P02 * c2 + p0;  // P C + p
@@ -359,15 +360,17 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
               ST* s = sp + (size_t)i * 8 * L;
               const double K00 = rg[t][0], K01 = rg[t][1], K02 = rg[t][2], K10 = rg[t][3];
               const double K11 = rg[t][4], K12 = rg[t][5], k0 = rg[t][6], k1 = rg[t][7];
-              if (i + kRing < N) {
+              {  // clamped loads: no branch, no register copies for the skipped case
+                const ST* sa = sp + (size_t)(i + kRing < N ? i + kRing : N - 1) * 8 * L;
 #pragma unroll
-                for (int e = 0; e < 8; e++) rg[t][e] = s[(kRing * 8 + e) * L];
+                for (int e = 0; e < 8; e++) rg[t][e] = sa[e * L];
               }
               const int old = old_n;
               const double rxi = rx, ryi = ry, rti = rt;
-              if (i + 1 < N) {  // next stage's state and reference, loaded a stage ahead
-                old_n = ap[(i + 1) * L];
-                ref(i + 1, rx, ry, rt);
+              {  // next stage's state and reference, loaded a stage ahead
+                const int inx = i + 1 < N ? i + 1 : N - 1;
+                old_n = ap[inx * L];
+                ref(inx, rx, ry, rt);
               }
               const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
               const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
@@ -391,18 +394,16 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                 // a fixed input sits exactly on its bound (k carries the bound, its K row is
                 // zero), so the HIK test reduces to the multiplier's sign for a fixed input and
                 // to the bound test for a free one
-                const bool nlo = (ca == 1) ? (g > 0.0) : (ca == 0 && u < lb);
-                const bool nhi = !nlo && ((ca == 2) ? (g < 0.0) : (ca == 0 && u > ub));
-                const int nca = nlo ? 1 : (nhi ? 2 : 0);
-                if (nca != ca && !(single && flipped)) {
-                  st = (st & ~(3 << (2 * a))) | (nca << (2 * a));
-                  flipped = true;
-                }
+                // (bitwise, every compare evaluated: no EXEC-masked region per input and stage)
+                const bool nlo = ((ca == 1) & (g > 0.0)) | ((ca == 0) & (u < lb));
+                const bool nhi = !nlo & (((ca == 2) & (g < 0.0)) | ((ca == 0) & (u > ub)));
+                const int nca = (int)nlo | ((int)nhi << 1);
+                const bool take = (nca != ca) & !(single & flipped);
+                st = take ? ((st & ~(3 << (2 * a))) | (nca << (2 * a))) : st;
+                flipped |= take;
               }
-              if (st != old) {
-                changed = true;
-                ap[i * L] = st;
-              }
+              changed |= (st != old);
+              ap[i * L] = st;  // unconditional: an unchanged state rewrites its own value
               const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
               const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;
               const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
