@@ -101,6 +101,7 @@ struct f110qp_ctx {
   int lane_mode = 0;         // lane scratch placement (LaneWork::mode)
   int lane_qpw = 0;          // lane QPs per wave (LaneWork::qpw, 0 = auto)
   int lane_rot = 1;          // lane heading-frame kernel when q0 == q1 (LaneWork::rot)
+  int lane_dref = 1;         // lane fp64 references in LDS when they fit (LaneWork::dref)
   hipStream_t stream = nullptr;
 };
 
@@ -186,6 +187,8 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
   }
   // test hook: F110QP_LANE_ROT=0 forces the lane back end's general-frame kernel
   if (const char* er = std::getenv("F110QP_LANE_ROT")) c->lane_rot = std::atoi(er) != 0;
+  // test hook: F110QP_LANE_DREF=0 keeps the lane back end's references as floats in LDS
+  if (const char* ed = std::getenv("F110QP_LANE_DREF")) c->lane_dref = std::atoi(ed) != 0;
   // test hook: F110QP_PDAS_MAX caps the wave kernel's box PDAS passes (0 = GI from scratch)
   k.pdas_max = 10;
   if (const char* ep = std::getenv("F110QP_PDAS_MAX")) {
@@ -270,6 +273,7 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   lw->mode = c->lane_mode;
   lw->qpw = c->lane_qpw;
   lw->rot = c->lane_rot;
+  lw->dref = c->lane_dref;
   return F110QP_OK;
 }
 

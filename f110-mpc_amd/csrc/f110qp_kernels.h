@@ -52,6 +52,7 @@ struct LaneWork {
   int mode = 0;   // scratch: 0 auto, 1 LDS fp64, 2 LDS fp32, 3 HBM fp64, 4 HBM fp32 (workspace)
   int qpw = 0;    // QPs per wave: 0 auto (lane_qps_per_wave), else a power of two <= 64
   int rot = 1;    // 1: heading-frame kernel when q0 == q1 (lane_kernel.h ROT); 0: general frame
+  int dref = 1;   // 1: fp64 references in LDS when the resident waves fit (DREF); 0: float
 };
 
 // waves the lane kernel's grid aims for (one per CU of the MI355X's 256)

@@ -78,7 +78,7 @@ constexpr int ring_depth() { return SLDS ? 2 : 4; }
 
 
 // Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
-template <typename ST, bool SLDS, int L, bool ROT>
+template <typename ST, bool SLDS, int L, bool ROT, bool DREF>
 __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                                                   const float* __restrict__ x0g,
                                                   const float* __restrict__ ulg,
@@ -90,6 +90,13 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
                                                   double* __restrict__ scr,
                                                   const WarmState ws, const int kmax) {
   extern __shared__ __attribute__((aligned(16))) float xr_s[];  // [3N][L] x_ref, transposed
+  // DREF: the references are kept as recentred (and, ROT, rotated) fp64 offsets [3N][L] at the
+  // start of LDS, converted once after staging; the float staging then sits in the upper half
+  // of that region (stage i's doubles end at byte 24 (i + 1) L, below the floats of stage i + 1
+  // at 12 N L + 12 (i + 1) L, so the in-order conversion never overwrites an unread float).
+  // Layout: DREF [3N][L] fp64 refs | (SLDS) scratch | [N][L] state; else [3N][L] float refs |
+  // [N][L] state | (SLDS) scratch.
+  float* const stg = DREF ? xr_s + 3 * P.N * L : xr_s;
   LSTAMP(t_start);
 #ifdef F110QP_STAMPS
   unsigned long long acc_bw = 0, acc_fw = 0, acc_out = 0, t_setup = 0, npass = 0;
@@ -132,7 +139,7 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
       }
 #pragma unroll
       for (int j = 0; j < kChunk; j++) {
-        if (dst[j] >= 0) xr_s[dst[j]] = vbuf[j];
+        if (dst[j] >= 0) stg[dst[j]] = vbuf[j];
         if (!isfinite(vbuf[j])) badq |= 1ull << (dst[j] & (L - 1));  // q = dst mod L
       }
     }
@@ -179,12 +186,16 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
   // scratch slot (i, e) of this QP: sp[(8 i + e) * L]; the PDAS state of stage i (2 bits
   // per input: 0 free, 1 lower bound, 2 upper bound) at ap[i * L].
   // LDS: [3N][L] references, [N][L] PDAS state, then (SLDS) the [N][8][L] Riccati scratch
-  int* ap = reinterpret_cast<int*>(xr_s + 3 * N * L) + slot;
+  double* const r64 = reinterpret_cast<double*>(xr_s) + slot;  // DREF only
   ST* sp;
+  int* ap;
   if constexpr (SLDS) {
-    sp = reinterpret_cast<ST*>(xr_s + 4 * N * L) + slot;
+    sp = reinterpret_cast<ST*>(xr_s + (DREF ? 6 : 4) * N * L) + slot;
+    ap = DREF ? reinterpret_cast<int*>(reinterpret_cast<ST*>(xr_s + 6 * N * L) + 8 * N * L) + slot
+              : reinterpret_cast<int*>(xr_s + 3 * N * L) + slot;
   } else {
     sp = reinterpret_cast<ST*>(scr) + (size_t)blockIdx.x * N * 8 * L + slot;
+    ap = reinterpret_cast<int*>(xr_s + (DREF ? 6 : 3) * N * L) + slot;
   }
   const int R = (2 * N + 63) / 64;  // register-row count of the wave kernel's act layout
   const unsigned kth = __float_as_uint(fTH0), kv = __float_as_uint(ulg[2 * b + 0]);
@@ -223,9 +234,10 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
       ap[i * L] = st;
     }
   }
-  auto ref = [&](int i, double& rx, double& ry, double& rt) {
-    const double dx = (double)xr_s[(3 * i + 0) * L + slot] - X0;
-    const double dy = (double)xr_s[(3 * i + 1) * L + slot] - Y0;
+  // recentred (ROT: rotated) reference of stage i from the float staging
+  auto ref_f = [&](int i, double& rx, double& ry, double& rt) {
+    const double dx = (double)stg[(3 * i + 0) * L + slot] - X0;
+    const double dy = (double)stg[(3 * i + 1) * L + slot] - Y0;
     if constexpr (ROT) {
       rx = cs * dx + sn * dy;
       ry = cs * dy - sn * dx;
@@ -233,7 +245,25 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
       rx = dx;
       ry = dy;
     }
-    rt = (double)xr_s[(3 * i + 2) * L + slot] - th0;
+    rt = (double)stg[(3 * i + 2) * L + slot] - th0;
+  };
+  if constexpr (DREF) {  // once per kernel instead of once per stage and sweep
+    for (int i = 0; i < N; i++) {
+      double rx, ry, rt;
+      ref_f(i, rx, ry, rt);
+      r64[(3 * i + 0) * L] = rx;
+      r64[(3 * i + 1) * L] = ry;
+      r64[(3 * i + 2) * L] = rt;
+    }
+  }
+  auto ref = [&](int i, double& rx, double& ry, double& rt) {
+    if constexpr (DREF) {
+      rx = r64[(3 * i + 0) * L];
+      ry = r64[(3 * i + 1) * L];
+      rt = r64[(3 * i + 2) * L];
+    } else {
+      ref_f(i, rx, ry, rt);
+    }
   };
 
   // non-finite data -> F110QP_NUMERICAL with NaN outputs (e.g. the planning stage's NaN x_ref
@@ -504,17 +534,17 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
 #endif
 }
 
-template <typename ST, bool SLDS, int L, bool ROT>
+template <typename ST, bool SLDS, int L, bool ROT, bool DREF>
 hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                          float* uo, float* xo, int* st, int* its, const WarmState& ws,
                          const LaneWork& lw, size_t lds, hipStream_t s) {
   const int waves = (B + L - 1) / L;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_kernel<ST, SLDS, L, ROT>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_kernel<ST, SLDS, L, ROT, DREF>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((lane_kernel<ST, SLDS, L, ROT>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr,
+  hipLaunchKernelGGL((lane_kernel<ST, SLDS, L, ROT, DREF>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr,
                      uo, xo, st, its, lw.scratch, ws, lw.kmax);
   return hipGetLastError();
 }

@@ -12,7 +12,7 @@
 namespace f110qp {
 
 #ifndef F110QP_LANE_ALL
-template <typename ST, bool SLDS, int L, bool ROT>
+template <typename ST, bool SLDS, int L, bool ROT, bool DREF>
 hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                          float* uo, float* xo, int* st, int* its, const WarmState& ws,
                          const LaneWork& lw, size_t lds, hipStream_t s);  // lane_inst.hip
@@ -27,14 +27,27 @@ int lane_qps_per_wave(int B, int qpw) {
   return L;
 }
 
-// the heading-frame variant when Q's (x, y) weights are equal (lane_kernel.h, ROT)
+// the heading-frame variant when Q's (x, y) weights are equal (lane_kernel.h, ROT), with the
+// references converted once to fp64 in LDS (DREF: 12 N L more bytes per wave than the float
+// references) when the grid runs one wave per CU. Measured: C4 shard 8,192 x N=40 195.8 ->
+// 184.6 us, C5 66.9 -> 65.3; at four waves per CU (65,536 x N=20) 107.0 -> 109.1, so not there.
+template <typename ST, bool SLDS, int L, bool DREF>
+static hipError_t launch_rot_d(const KParams& P, int B, const float* x0, const float* ul,
+                               const float* xr, float* uo, float* xo, int* st, int* its,
+                               const WarmState& ws, const LaneWork& lw, size_t lds, hipStream_t s) {
+  if (lw.rot && P.q[0] == P.q[1])
+    return launch_lane_t<ST, SLDS, L, true, DREF>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
+  return launch_lane_t<ST, SLDS, L, false, DREF>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
+}
 template <typename ST, bool SLDS, int L>
 static hipError_t launch_rot(const KParams& P, int B, const float* x0, const float* ul,
                              const float* xr, float* uo, float* xo, int* st, int* its,
                              const WarmState& ws, const LaneWork& lw, size_t lds, hipStream_t s) {
-  if (lw.rot && P.q[0] == P.q[1])
-    return launch_lane_t<ST, SLDS, L, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
-  return launch_lane_t<ST, SLDS, L, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
+  const size_t ldsd = lds + (size_t)P.N * L * 12;
+  const size_t per_cu = (((size_t)B + L - 1) / L + 255) / 256;
+  if (lw.dref && per_cu == 1 && ldsd <= 160 * 1024)
+    return launch_rot_d<ST, SLDS, L, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, ldsd, s);
+  return launch_rot_d<ST, SLDS, L, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
 }
 
 template <int L>

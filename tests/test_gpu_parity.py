@@ -455,14 +455,18 @@ def test_lane_backend_custom_weights_and_far_origin(oracle, capi, be):
     assert rel_err(u, ur).max() <= TOL and rel_err(x, xr).max() <= TOL
 
 
+@pytest.mark.parametrize("dref", ["0", "1"])
 @pytest.mark.parametrize("rot", ["0", "1"])
 @pytest.mark.parametrize("N", [20, 40])
-def test_lane_backend_heading_frame(oracle, capi, monkeypatch, rot, N):
+def test_lane_backend_heading_frame(oracle, capi, monkeypatch, rot, dref, N):
     """q0 == q1 (the shipped params.yaml) runs the lane kernel in the frame of the heading
     theta0 (lane_kernel.h ROT: four zero model entries); F110QP_LANE_ROT=0 forces the general
-    frame. Both give the exact optimum, also 1 km from the origin with headings all round the
-    circle, and agree with each other."""
+    frame. The references are converted once to fp64 offsets in LDS (DREF) where the resident
+    waves fit; F110QP_LANE_DREF=0 keeps the per-stage conversion of the float staging. Every
+    combination gives the exact optimum, also 1 km from the origin with headings all round the
+    circle."""
     monkeypatch.setenv("F110QP_LANE_ROT", rot)
+    monkeypatch.setenv("F110QP_LANE_DREF", dref)
     w = workload.make_batch(1500, N, seed=6060 + N, heading="true", lateral=1.5, steer_range=1.0)
     w["x0"][:, 2] = np.random.default_rng(N).uniform(-np.pi, np.pi, 1500).astype(np.float32)
     w["x0"][:, :2] += np.float32(1000.0)
