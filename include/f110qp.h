@@ -71,14 +71,14 @@ extern "C" {
 #define F110QP_BACKEND_WAVE 1     /* one wavefront per QP: condensed W = H^-1 + PDAS/GI         */
 #define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64 (box rows only;      */
                                   /* gap rows always use the wave back end)                    */
-/* AUTO thresholds, measured on MI355X (kernel us). N = 20: wave 78 vs lane 88
- * at 4,096 cold QPs of the C2 recipe, but lane 80 vs wave 100 on the C5 stream's cold tick and
- * 39 vs 91 warm; 141 vs 91 at 8,192. N = 30: crossover near 3,800. N = 40: wave 105 vs lane 200
- * at 512, 194 vs 201 at 1,024, lane beyond. Grouped calls use the same thresholds: the wave back
+/* AUTO thresholds, measured on MI355X (kernel us, DESIGN.md section 6, after the heading-frame /
+ * branch-free lane kernel). N = 20 (C2 recipe, cold): wave 66.0 vs lane 69.8 at 3,072, 83.4 vs
+ * 70.1 at 4,096; the C5 stream's cold tick at 4,096: lane 62 vs wave 80. N = 30: 121 vs 103 at
+ * 3,072. N = 40: wave 107 vs lane 151 at 512, 183 vs 176 at 768, 199 vs 153 at 1,024. Grouped calls use the same thresholds: the wave back
  * end's per-group W saves its inverse but its per-QP active-set phase still dominates (C4
  * candidate sets: 8,192 x N=40 grouped wave 1,041 us vs lane 240 us). */
-#define F110QP_LANE_MIN_BATCH 4096
-#define F110QP_LANE_MIN_BATCH_WIDE 1025
+#define F110QP_LANE_MIN_BATCH 3072
+#define F110QP_LANE_MIN_BATCH_WIDE 768
 #define F110QP_LANE_MIN_BATCH_GROUPED F110QP_LANE_MIN_BATCH
 #define F110QP_LANE_MIN_BATCH_GROUPED_WIDE F110QP_LANE_MIN_BATCH_WIDE
 

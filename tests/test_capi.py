@@ -111,12 +111,14 @@ def test_capi_raises_when_library_missing(monkeypatch):
 
 def test_auto_backend_policy(capi):
     """BACKEND_AUTO: the wave kernel for small box batches and for gap rows, the lane kernel
-    from the measured crossover (4,096 QPs at N <= 32; above 1,024 at N > 32)."""
+    from the measured crossover (3,072 QPs at N <= 32; 768 at N > 32)."""
     assert capi.auto_backend(20, 1024, False) == capi.BACKEND_WAVE
+    assert capi.auto_backend(20, 3071, False) == capi.BACKEND_WAVE
+    assert capi.auto_backend(20, 3072, False) == capi.BACKEND_LANE
     assert capi.auto_backend(20, 4096, False) == capi.BACKEND_LANE
     assert capi.auto_backend(20, 65536, True) == capi.BACKEND_WAVE
-    assert capi.auto_backend(40, 1025, False) == capi.BACKEND_LANE
-    assert capi.auto_backend(40, 1024, False) == capi.BACKEND_WAVE
+    assert capi.auto_backend(40, 768, False) == capi.BACKEND_LANE
+    assert capi.auto_backend(40, 767, False) == capi.BACKEND_WAVE
 
 
 def test_auto_backend_grouped_policy(capi):
@@ -124,8 +126,8 @@ def test_auto_backend_grouped_policy(capi):
     C4 batch run on the lane kernel (grouped wave measured 1,041 vs 240 us at the shard)."""
     assert capi.auto_backend(40, 8192, False, grouped=True) == capi.BACKEND_LANE
     assert capi.auto_backend(40, 65536, False, grouped=True) == capi.BACKEND_LANE
-    assert capi.auto_backend(40, 1024, False, grouped=True) == capi.BACKEND_WAVE
-    assert capi.auto_backend(20, 4095, False, grouped=True) == capi.BACKEND_WAVE
+    assert capi.auto_backend(40, 767, False, grouped=True) == capi.BACKEND_WAVE
+    assert capi.auto_backend(20, 3071, False, grouped=True) == capi.BACKEND_WAVE
 
 
 def test_qp_dims_match_reference_sizes(capi, oracle):
