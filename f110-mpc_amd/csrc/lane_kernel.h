@@ -73,8 +73,14 @@ __device__ unsigned long long g_lstamps[4096 * kLaneStampSlots];  // one TU per 
 
 // stages of scratch loaded ahead in the forward and output sweeps: HBM latency is several
 // stages of compute, LDS latency (~60 cycles at one wave per SIMD) less than one
+#ifndef F110QP_LANE_RING_LDS
+#define F110QP_LANE_RING_LDS 2
+#endif
+#ifndef F110QP_LANE_NEWTON
+#define F110QP_LANE_NEWTON 2  // Newton steps after v_rcp_f64 in the masked 2x2 inverse
+#endif
 template <bool SLDS>
-constexpr int ring_depth() { return SLDS ? 2 : 4; }
+constexpr int ring_depth() { return SLDS ? F110QP_LANE_RING_LDS : 4; }
 
 
 // Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
@@ -339,8 +345,8 @@ __global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
         const double M00 = f0 ? H00 : 1.0, M11 = f1 ? H11 : 1.0, M01 = (f0 && f1) ? H01 : 0.0;
         const double det = M00 * M11 - M01 * M01;  // > 0: R + B'PB is positive definite
         double idet = __builtin_amdgcn_rcp(det);   // + two Newton steps: full fp64
-        idet = fma(idet, fma(-det, idet, 1.0), idet);
-        idet = fma(idet, fma(-det, idet, 1.0), idet);
+#pragma unroll
+        for (int nt = 0; nt < F110QP_LANE_NEWTON; nt++) idet = fma(idet, fma(-det, idet, 1.0), idet);
         const double I00 = f0 ? M11 * idet : 0.0, I11 = f1 ? M00 * idet : 0.0;
         const double I01 = (f0 && f1) ? -M01 * idet : 0.0;
         const double K00 = -I00 * X00 - I01 * X10, K01 = -I00 * X01 - I01 * X11;
