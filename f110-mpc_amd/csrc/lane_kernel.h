@@ -74,13 +74,16 @@ __device__ unsigned long long g_lstamps[4096 * kLaneStampSlots];  // one TU per 
 // stages of scratch loaded ahead in the forward and output sweeps: HBM latency is several
 // stages of compute, LDS latency (~60 cycles at one wave per SIMD) less than one
 #ifndef F110QP_LANE_RING_LDS
-#define F110QP_LANE_RING_LDS 2
+#define F110QP_LANE_RING_LDS 1  // measured: 1 vs 2 stages ahead, C4 shard 184.3 -> 178.9 us, C5 64.6 -> 61.5
+#endif
+#ifndef F110QP_LANE_RING_HBM
+#define F110QP_LANE_RING_HBM 4
 #endif
 #ifndef F110QP_LANE_NEWTON
 #define F110QP_LANE_NEWTON 2  // Newton steps after v_rcp_f64 in the masked 2x2 inverse
 #endif
 template <bool SLDS>
-constexpr int ring_depth() { return SLDS ? F110QP_LANE_RING_LDS : 4; }
+constexpr int ring_depth() { return SLDS ? F110QP_LANE_RING_LDS : F110QP_LANE_RING_HBM; }
 
 
 // Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
