@@ -87,8 +87,17 @@ constexpr int ring_depth() { return SLDS ? F110QP_LANE_RING_LDS : F110QP_LANE_RI
 
 
 // Scratch of the Riccati passes: ST = double or float, in LDS (SLDS) or in the HBM workspace.
+// Occupancy hint for the register allocator / scheduler: 2 waves per SIMD for the LDS-scratch
+// kernels (the grid still runs one wave per SIMD or CU; the 256-VGPR budget gave a better
+// schedule: C4 shard 179.2 -> 172.4 us, C5 61.1 -> 60.0), 1 for the HBM-scratch ones (2
+// measured C4 248.9 -> 251.7). F110QP_LANE_WPE overrides both (measurement knob).
+#ifdef F110QP_LANE_WPE
+#define F110QP_LANE_ATTR __attribute__((amdgpu_waves_per_eu(F110QP_LANE_WPE, F110QP_LANE_WPE)))
+#else
+#define F110QP_LANE_ATTR __attribute__((amdgpu_waves_per_eu(SLDS ? 2 : 1, SLDS ? 2 : 1)))
+#endif
 template <typename ST, bool SLDS, int L, bool ROT, bool DREF>
-__global__ __launch_bounds__(64) void lane_kernel(const KParams P, const int B,
+__global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams P, const int B,
                                                   const float* __restrict__ x0g,
                                                   const float* __restrict__ ulg,
                                                   const float* __restrict__ xrg,
