@@ -18,8 +18,8 @@
 //                         the masked problem. The gradient R(u_i - u_des) + B' lambda_{i+1}
 //                         gives the bound multipliers and the PDAS re-guess of stage i.
 // A forward sweep that changes nothing certifies the KKT conditions (active bounds with
-// non-negative multipliers, inactive inputs inside the box); its u_i (kept in the scratch)
-// roll out to x* in a last output sweep. Everything is fp64 in registers, recentred on
+// non-negative multipliers, inactive inputs inside the box); its gains (kept in the scratch)
+// give u* and x* in a last output sweep. Everything is fp64 in registers, recentred on
 // (x0, y0, theta0) like the wave kernel, so the result is the exact optimum to ~1e-12 (to
 // ~1e-7 with fp32 scratch).
 //
@@ -38,7 +38,7 @@
 // waits for the maximum pass count of fewer QPs. The wave's L
 // reference paths are contiguous in HBM; they are staged once into LDS transposed ([i][c][L],
 // conflict free), every load of the wave in flight at once. K_i, k_i (backward -> forward; u_i
-// overwrites K_i's first two slots in the forward) go through a per-wave scratch [stage][8][L]
+// are recomputed from them in the output sweep) go through a per-wave scratch [stage][8][L]
 // in LDS when the resident waves fit, else in an HBM workspace read through a prefetch ring;
 // the per-stage PDAS state sits in LDS. No cross-lane traffic at all except the wave-uniform
 // "any lane still iterating" vote.
@@ -437,7 +437,6 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
                 }
                 const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
                 const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
-                s[0] = (ST)u0; s[L] = (ST)u1;  // the solution if this sweep changes nothing
                 // lambda_{i+1} = (I - E')(lambda_i - Q(x_i - r_i))
                 const double w0 = l0 - q0 * (x0 - rxi), w1 = l1 - q1 * (x1 - ryi);
                 const double w2 = l2 - q2 * (x2 - rti);
@@ -519,7 +518,6 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
                 }
                 const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
                 const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
-                s[0] = (ST)u0; s[L] = (ST)u1;  // the solution if this sweep changes nothing
                 // lambda_{i+1} = (I - E')(lambda_i - Q(x_i - r_i))
                 const double w0 = l0 - q0 * (x0 - rxi), w1 = l1 - q1 * (x1 - ryi);
                 const double w2 = l2 - q2 * (x2 - rti);
@@ -559,7 +557,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
         }
       }
       LACC(acc_fw, t_fw);
-      if (!changed && !done) {  // KKT point: the u_i of this sweep (in the scratch) are u*
+      if (!changed && !done) {  // KKT point: the gains of this pass (in the scratch) give u*
         done = true;
         iters = pass + 1;  // equality-QP solves incl. the confirming one
       }
@@ -577,22 +575,32 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
       xo[1] = solved ? x0g[3 * b + 1] : nanv;
       xo[2] = solved ? fTH0 : nanv;
     }
+    // u* = K_i x_i + k_i from the gains of the last backward sweep (the set of the converged
+    // pass: a converged lane's later sweeps rewrote the same gains), the same expression the
+    // forward sweep evaluated — so the forward sweeps store no u (2 of 10 scratch values per
+    // stage and pass) and this sweep reads the 8 gains once.
     double x0 = 0.0, x1 = 0.0, x2 = 0.0;
-    ST ur[kRing][2];
+    ST ur[kRing][8];
 #pragma unroll
     for (int t = 0; t < kRing; t++)
-      if (t < N) { ur[t][0] = sp[(size_t)t * 8 * L]; ur[t][1] = sp[(size_t)t * 8 * L + L]; }
+      if (t < N) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) ur[t][e] = sp[((size_t)t * 8 + e) * L];
+      }
     for (int i0 = 0; i0 < N; i0 += kRing) {
 #pragma unroll
       for (int t = 0; t < kRing; t++) {
         const int i = i0 + t;
         if (i < N) {
-          const double u0 = (double)ur[t][0], u1 = (double)ur[t][1];
+          const double K00 = ur[t][0], K01 = ur[t][1], K02 = ur[t][2], K10 = ur[t][3];
+          const double K11 = ur[t][4], K12 = ur[t][5], k0 = ur[t][6], k1 = ur[t][7];
           if (i + kRing < N) {
             const ST* s = sp + (size_t)(i + kRing) * 8 * L;
-            ur[t][0] = s[0];
-            ur[t][1] = s[L];
+#pragma unroll
+            for (int e = 0; e < 8; e++) ur[t][e] = s[e * L];
           }
+          const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
+          const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
           const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
           const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;
           const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
