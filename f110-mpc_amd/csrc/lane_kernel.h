@@ -38,8 +38,9 @@
 // waits for the maximum pass count of fewer QPs. The wave's L
 // reference paths are contiguous in HBM; they are staged once into LDS transposed ([i][c][L],
 // conflict free), every load of the wave in flight at once. K_i, k_i (backward -> forward; u_i
-// are recomputed from them in the output sweep) go through a per-wave scratch [stage][8][L]
-// in LDS when the resident waves fit, else in an HBM workspace read through a prefetch ring;
+// are recomputed from them in the output sweep) go through a per-wave scratch, [stage][8][L]
+// in LDS when the resident waves fit, else [stage][L][8] in an HBM workspace read through a
+// prefetch ring;
 // the per-stage PDAS state sits in LDS. No cross-lane traffic at all except the wave-uniform
 // "any lane still iterating" vote.
 // Convergence: PDAS (every violated complementarity condition flips at once) for kmax passes;
@@ -206,10 +207,12 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
   const double lb0 = (double)P.umin[0], lb1 = (double)P.umin[1];
   const double ub0 = (double)P.umax[0], ub1 = (double)P.umax[1];
 
-  // scratch slot (i, e) of this QP: sp[(8 i + e) * L]; the PDAS state of stage i (2 bits
+  // scratch slot (i, e) of this QP: sp[8 L i + e ES] (LDS [stage][8][L]: ES = L; HBM
+  // [stage][L][8]: ES = 1); the PDAS state of stage i (2 bits
   // per input: 0 free, 1 lower bound, 2 upper bound) at ap[i * L].
   // LDS: [3N][L] references, [N][L] PDAS state, then (SLDS) the [N][8][L] Riccati scratch
   double* const r64 = reinterpret_cast<double*>(xr_s) + slot;  // DREF only
+  constexpr int ES = SLDS ? L : 1;  // stride of a stage's 8 gains in the scratch
   ST* sp;
   int* ap;
   if constexpr (SLDS) {
@@ -217,7 +220,10 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
     ap = DREF ? reinterpret_cast<int*>(reinterpret_cast<ST*>(xr_s + 6 * N * L) + 8 * N * L) + slot
               : reinterpret_cast<int*>(xr_s + 3 * N * L) + slot;
   } else {
-    sp = reinterpret_cast<ST*>(scr) + (size_t)blockIdx.x * N * 8 * L + slot;
+    // HBM: [stage][lane][8], a lane's 8 gains contiguous (two or four 16-B accesses per stage
+    // instead of eight 4/8-B ones; 32-B aligned: the workspace is hipMalloc'ed)
+    sp = static_cast<ST*>(__builtin_assume_aligned(
+        reinterpret_cast<ST*>(scr) + (size_t)blockIdx.x * N * 8 * L + (size_t)slot * 8, 32));
     ap = reinterpret_cast<int*>(xr_s + (DREF ? 6 : 3) * N * L) + slot;
   }
   const int R = (2 * N + 63) / 64;  // register-row count of the wave kernel's act layout
@@ -372,8 +378,8 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
         const double K12 = -I01 * X02 - I11 * X12;
         const double w0 = h0 + H00 * bA0 + H01 * bA1, w1 = h1 + H01 * bA0 + H11 * bA1;
         const double k0 = bA0 - (I00 * w0 + I01 * w1), k1 = bA1 - (I01 * w0 + I11 * w1);
-        s[0] = (ST)K00; s[L] = (ST)K01; s[2 * L] = (ST)K02; s[3 * L] = (ST)K10; s[4 * L] = (ST)K11;
-        s[5 * L] = (ST)K12; s[6 * L] = (ST)k0; s[7 * L] = (ST)k1;
+        s[0] = (ST)K00; s[ES] = (ST)K01; s[2 * ES] = (ST)K02; s[3 * ES] = (ST)K10;
+        s[4 * ES] = (ST)K11; s[5 * ES] = (ST)K12; s[6 * ES] = (ST)k0; s[7 * ES] = (ST)k1;
         // V_i: P = Hxx + Hux' K, p = hx + Hux' k
         P00 = Y00 + X00 * K00 + X10 * K10;
         P01 = Y01 + X00 * K01 + X10 * K11;
@@ -410,7 +416,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
           for (int t = 0; t < kRing; t++)
             if (t < N) {
   #pragma unroll
-              for (int e = 0; e < 8; e++) rg[t][e] = sp[((size_t)t * 8 + e) * L];
+              for (int e = 0; e < 8; e++) rg[t][e] = sp[(size_t)t * 8 * L + e * ES];
             }
           double rx, ry, rt;
           ref(0, rx, ry, rt);
@@ -426,7 +432,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
                 {  // clamped loads: no branch, no register copies for the skipped case
                   const ST* sa = sp + (size_t)(i + kRing < N ? i + kRing : N - 1) * 8 * L;
   #pragma unroll
-                  for (int e = 0; e < 8; e++) rg[t][e] = sa[e * L];
+                  for (int e = 0; e < 8; e++) rg[t][e] = sa[e * ES];
                 }
                 const int old = old_n;
                 const double rxi = rx, ryi = ry, rti = rt;
@@ -491,7 +497,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
           for (int t = 0; t < kRing; t++)
             if (t < N) {
   #pragma unroll
-              for (int e = 0; e < 8; e++) rg[t][e] = sp[((size_t)t * 8 + e) * L];
+              for (int e = 0; e < 8; e++) rg[t][e] = sp[(size_t)t * 8 * L + e * ES];
             }
           double rx, ry, rt;
           ref(0, rx, ry, rt);
@@ -507,7 +513,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
                 {  // clamped loads: no branch, no register copies for the skipped case
                   const ST* sa = sp + (size_t)(i + kRing < N ? i + kRing : N - 1) * 8 * L;
   #pragma unroll
-                  for (int e = 0; e < 8; e++) rg[t][e] = sa[e * L];
+                  for (int e = 0; e < 8; e++) rg[t][e] = sa[e * ES];
                 }
                 const int old = old_n;
                 const double rxi = rx, ryi = ry, rti = rt;
@@ -585,7 +591,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
     for (int t = 0; t < kRing; t++)
       if (t < N) {
 #pragma unroll
-        for (int e = 0; e < 8; e++) ur[t][e] = sp[((size_t)t * 8 + e) * L];
+        for (int e = 0; e < 8; e++) ur[t][e] = sp[(size_t)t * 8 * L + e * ES];
       }
     for (int i0 = 0; i0 < N; i0 += kRing) {
 #pragma unroll
@@ -597,7 +603,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
           if (i + kRing < N) {
             const ST* s = sp + (size_t)(i + kRing) * 8 * L;
 #pragma unroll
-            for (int e = 0; e < 8; e++) ur[t][e] = s[e * L];
+            for (int e = 0; e < 8; e++) ur[t][e] = s[e * ES];
           }
           const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
           const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
