@@ -1592,7 +1592,12 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 // One QP per workgroup (= one wave). With `list` the grid walks the index list instead
 // (count read on the device): the lane-per-QP kernel hands its non-converged QPs over this way.
 template <int NUM, bool GAP>
-__global__ __launch_bounds__(64) void solve_kernel(const KParams P, const int B,
+#ifdef F110QP_SOLVE_WPE  // measurement knob: occupancy hint for the register allocator
+#define F110QP_SOLVE_ATTR __attribute__((amdgpu_waves_per_eu(F110QP_SOLVE_WPE, F110QP_SOLVE_WPE)))
+#else
+#define F110QP_SOLVE_ATTR
+#endif
+__global__ __launch_bounds__(64) F110QP_SOLVE_ATTR void solve_kernel(const KParams P, const int B,
                                                    const float* __restrict__ x0g,
                                                    const float* __restrict__ ulg,
                                                    const float* __restrict__ xrg,
