@@ -1,3 +1,4 @@
+# Host diagnostic; it imports the CPU oracle, so it lives under tests/ (test infrastructure).
 # Active-row census of the bench C3 batch on the CPU oracle; host only.
 import sys, numpy as np
 sys.path.insert(0, "f110-mpc_amd"); sys.path.insert(0, ".")
