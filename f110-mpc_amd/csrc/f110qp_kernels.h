@@ -44,7 +44,7 @@ struct WarmState {
   int ngroups = 0;
 };
 
-// Workspace of the lane-per-QP kernel (lane_kernel.hip): the HBM Riccati scratch when it does
+// Workspace of the lane-per-QP kernel (lane_kernel.h): the HBM Riccati scratch when it does
 // not stay in LDS (ceil(B/L) x N x 8 x L doubles at most, L QPs per wave <= 64).
 struct LaneWork {
   double* scratch = nullptr;

@@ -1,4 +1,4 @@
-// lane_kernel.hip — the throughput path: ONE LANE PER QP (up to 64 box-constrained QPs per wave).
+// lane_kernel.h — the throughput path: ONE LANE PER QP (up to 64 box-constrained QPs per wave).
 //
 // The reference solves, per control tick, the sparse QP of MPC::Update (src/mpc.cpp:69-143):
 // min sum_i 1/2 |x_i - r_i|_Q^2 + 1/2 |u_i - u_des|_R^2 subject to the dynamics rows
