@@ -121,7 +121,20 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int, c1_ticks: int):
+def _admm_rate(oracle, prm, st, w, hs, gap, threads, seconds, B):
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        _, stat, its = oracle.admm_solve_batch(prm, st, w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=gap,
+                                               num_threads=threads)
+        n += B
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return n, el, stat, its
+
+
+def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int, c1_ticks: int,
+                 full_threads: int = 0):
     """Time the reference's algorithm on the host cores: oracle/osqp_admm.c, a restatement of
     OSQP 0.6 with the settings MPC::Update uses (defaults + warm start; mpc.cpp:98-133) on the
     reference's own sparse QP (re-scaled and re-factored per tick, as OSQP must when A changes).
@@ -141,15 +154,15 @@ def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int, c
     st = oracle.admm_settings()
     oracle.admm_solve_batch(prm, st, w["x0"][:64], w["u_lin"][:64], w["x_ref"][:64],
                             None if hs is None else hs[:64], gap_active=gap, num_threads=threads)
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        _, stat, its = oracle.admm_solve_batch(prm, st, w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=gap,
-                                               num_threads=threads)
-        n += B
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+    n, el, stat, its = _admm_rate(oracle, prm, st, w, hs, gap, threads, seconds, B)
+    # the same over every CPU this process may run on (all host cores), when the
+    # per-GPU share (OMP_NUM_THREADS on the GPU box) is smaller than that
+    full = None
+    if full_threads > threads:
+        nf, elf, _, _ = _admm_rate(oracle, prm, st, w, hs, gap, full_threads, max(3.0, seconds / 3), B)
+        full = {"value": nf / elf, "unit": "QP solves/s", "cores": full_threads,
+                "sample": f"{nf} QPs ({nf // B} x {B} {config} ticks) in {elf:.1f} s, same solver, "
+                          f"OpenMP over {full_threads} threads (every CPU in this process's affinity mask)"}
     # the exact solver (the parity oracle) on the same sample, for reference
     n2 = 0
     t1 = time.perf_counter()
@@ -172,7 +185,7 @@ def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int, c
                         "qps_one_core": float(1e6 / us.mean())}
         c1["note"] = ("C1 = BASELINE configs[0]: single horizon-20 QP per tick on one core (calling thread), "
                       "wall time of the whole solve per tick; instances cycle over 1,024 seeded ticks")
-    return dict(value=n / el, unit="QP solves/s", cores=threads, kind="port",
+    out = dict(value=n / el, unit="QP solves/s", cores=threads, kind="port",
                 host={"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
                       "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "cpu_model": cpu_model(),
                       "threads_used": threads},
@@ -182,6 +195,11 @@ def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int, c
                        f"eps=1e-3, check every 25, banded LDL' KKT) with OpenMP over QPs; mean ADMM iters "
                        f"{float(np.mean(its)):.1f}, solved {float(np.mean(stat == 1)):.3f}",
                 exact_oracle_qps=n2 / el2)
+    if full is not None:
+        out["full_host"] = full
+        out["note"] = (f"value/cores = the per-GPU CPU share ({threads} threads = OMP_NUM_THREADS on the GPU box); "
+                       f"full_host = all {full_threads} CPUs of the affinity mask")
+    return out
 
 
 def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
@@ -254,6 +272,8 @@ def main():
                          "OMP_NUM_THREADS when set)")
     ap.add_argument("--c1-ticks", type=int, default=10000, help="single-core C1 ticks per solver (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-full-host", action="store_true",
+                    help="skip the all-CPUs leg of the CPU baseline (the per-GPU share is always timed)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, one GPU per rank); gloo only to rehearse several "
                          "ranks on fewer GPUs (ranks share devices round robin)")
@@ -263,7 +283,8 @@ def main():
                     help="grouped solve (one W = H^-1 per 120-candidate scenario, f110qp_solve_grouped_dev); "
                          "auto = on for c4")
     ap.add_argument("--backend", default="auto", choices=["auto", "wave", "lane"],
-                    help="solver back end (auto: lane-per-QP for box-only batches >= 2048)")
+                    help="solver back end (auto: lane-per-QP for box-only batches >= capi.LANE_MIN_BATCH = 3072 "
+                         "at N <= 32, >= capi.LANE_MIN_BATCH_WIDE = 768 at N > 32; f110qp_backend_info)")
     args = ap.parse_args()
 
     import torch
@@ -368,9 +389,15 @@ def main():
             gid_np = np.arange(Bper, dtype=np.int32)
         gid = torch.from_numpy(gid_np).to(dev)
         ngroups = int(gid_np.max()) + 1
-    eff = capi.auto_backend(N, Bper, gap, grouped) if backend == capi.BACKEND_AUTO else backend
-    be_name = "lane" if (eff == capi.BACKEND_LANE and not gap) else "wave"
     solver = capi.Solver(cfg)
+    # the launch this call makes, as the library resolves it (back end, QPs per wave, scratch)
+    eff, lane_qpw, lane_scr = solver.backend_info(Bper, grouped)
+    be_name = "lane" if eff == capi.BACKEND_LANE else "wave"
+    if be_name == "lane":
+        dtype = "fp64" if lane_scr in (1, 3) else "fp64 (fp32 Riccati-gain scratch in " + (
+            "LDS)" if lane_scr == 2 else "HBM)")
+    else:
+        dtype = "fp32 (fp64 refinement and re-check)"
     stream = torch.cuda.current_stream(dev)
     tick = [0]
 
@@ -501,7 +528,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
-        "dtype": "fp32 (fp64 refinement)",
+        "dtype": dtype,
         "data": "synthetic (seeded; SURVEY.md 8(d) recipe: simulate_dynamics mini paths)",
         "config": {
             "workload": desc,
@@ -512,6 +539,8 @@ def main():
             "warm_start": bool(warm),
             "backend": {"wave": "wave-per-QP (condensed, PDAS/GI)", "lane": "lane-per-QP (Riccati/PDAS fp64)"}[be_name]
                        + (" grouped: one W = H^-1 per scenario" if grouped and be_name == "wave" else ""),
+            **({"lane_qps_per_wave": lane_qpw, "lane_scratch": capi.SCRATCH_NAMES[lane_scr]}
+               if be_name == "lane" else {}),
             "parallelism": f"independent QP shards x{world} (no collective)"
                            + (f", scenario-aligned ({GROUP}) split of one global batch" if strong else ""),
             "solved_fraction": solved,
@@ -554,7 +583,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config, N, gap, args.cpu_seconds,
-                                               args.cpu_threads or cpu_threads_default(), args.c1_ticks)
+                                               args.cpu_threads or cpu_threads_default(), args.c1_ticks,
+                                               full_threads=0 if args.no_full_host else len(os.sched_getaffinity(0)))
         except Exception as e:  # the baseline must never take the GPU number down
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:

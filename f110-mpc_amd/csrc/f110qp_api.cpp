@@ -286,6 +286,12 @@ int f110qp_warm_reset(f110qp_ctx* c) {
 int f110qp_solve_batch_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                            const float* xr, const float* hs, float* uo, float* xo, int* st,
                            int* it, void* stream) {
+  return f110qp_solve_batch_ex_dev(c, batch, x0, ul, xr, hs, uo, xo, st, it, nullptr, nullptr, stream);
+}
+
+int f110qp_solve_batch_ex_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                              const float* xr, const float* hs, float* uo, float* xo, int* st,
+                              int* it, double* obj, double* cost, void* stream) {
   int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
   if (rc || batch == 0) return rc;
   const float* h = (c->cfg.gap_mode == F110QP_GAP_ACTIVE) ? hs : nullptr;
@@ -296,8 +302,11 @@ int f110qp_solve_batch_dev(f110qp_ctx* c, int batch, const float* x0, const floa
   f110qp::LaneWork lw;
   rc = lane_work(c, batch, (hipStream_t)stream, &backend, &lw);
   if (rc) return rc;
+  f110qp::ObjOut oo;
+  oo.obj = obj;
+  oo.cost = cost;
   hipError_t e = f110qp::launch_solve(c->kp, batch, x0, ul, xr, h, uo, xo, st, it, ws, backend,
-                                      lw, (hipStream_t)stream);
+                                      lw, oo, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
   return F110QP_OK;
 }
@@ -328,6 +337,14 @@ static int check_groups(const int* group, int num_groups, int batch) {
 int f110qp_solve_grouped_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                              const float* xr, const float* hs, const int* group, int num_groups,
                              float* uo, float* xo, int* st, int* it, void* stream) {
+  return f110qp_solve_grouped_ex_dev(c, batch, x0, ul, xr, hs, group, num_groups, uo, xo, st, it,
+                                     nullptr, nullptr, stream);
+}
+
+int f110qp_solve_grouped_ex_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                                const float* xr, const float* hs, const int* group, int num_groups,
+                                float* uo, float* xo, int* st, int* it, double* obj, double* cost,
+                                void* stream) {
   int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
   if (rc || batch == 0) return rc;
   if ((rc = check_groups(group, num_groups, batch))) return rc;
@@ -338,37 +355,88 @@ int f110qp_solve_grouped_dev(f110qp_ctx* c, int batch, const float* x0, const fl
   int backend;
   f110qp::LaneWork lw;
   if ((rc = lane_work(c, batch, (hipStream_t)stream, &backend, &lw, true))) return rc;
+  f110qp::ObjOut oo;
+  oo.obj = obj;
+  oo.cost = cost;
   hipError_t e = f110qp::launch_solve_grouped(c->kp, batch, x0, ul, xr, h, uo, xo, st, it, gws,
-                                              leader, backend, lw, (hipStream_t)stream);
+                                              leader, backend, lw, oo, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(e, "grouped solve launch");
   return F110QP_OK;
 }
 
 static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul, const float* xr,
                       const float* hs, const int* group, int num_groups, float* uo, float* xo,
-                      int* st, int* it);
+                      int* st, int* it, double* obj, double* cost);
 
 int f110qp_solve_batch(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                        const float* xr, const float* hs, float* uo, float* xo, int* st,
                        int* it) {
-  return solve_host(c, batch, x0, ul, xr, hs, nullptr, 0, uo, xo, st, it);
+  return solve_host(c, batch, x0, ul, xr, hs, nullptr, 0, uo, xo, st, it, nullptr, nullptr);
+}
+
+int f110qp_solve_batch_ex(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                          const float* xr, const float* hs, float* uo, float* xo, int* st,
+                          int* it, double* obj, double* cost) {
+  return solve_host(c, batch, x0, ul, xr, hs, nullptr, 0, uo, xo, st, it, obj, cost);
 }
 
 int f110qp_solve_grouped(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                          const float* xr, const float* hs, const int* group, int num_groups,
                          float* uo, float* xo, int* st, int* it) {
+  return f110qp_solve_grouped_ex(c, batch, x0, ul, xr, hs, group, num_groups, uo, xo, st, it,
+                                 nullptr, nullptr);
+}
+
+int f110qp_solve_grouped_ex(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                            const float* xr, const float* hs, const int* group, int num_groups,
+                            float* uo, float* xo, int* st, int* it, double* obj, double* cost) {
   if (batch > 0) {
     const int rc = check_groups(group, num_groups, batch);
     if (rc) return rc;
   }
-  return solve_host(c, batch, x0, ul, xr, hs, group, num_groups, uo, xo, st, it);
+  return solve_host(c, batch, x0, ul, xr, hs, group, num_groups, uo, xo, st, it, obj, cost);
+}
+
+int f110qp_backend_info(f110qp_ctx* c, int batch, int grouped, int* backend, int* qps_per_wave,
+                        int* scratch) {
+  if (!c) return fail(F110QP_ERR_INVALID, "ctx is NULL");
+  if (batch < 1) return fail(F110QP_ERR_INVALID, "batch must be >= 1");
+  const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
+  int be = c->cfg.backend;
+  if (be == F110QP_BACKEND_AUTO) {
+    const int min_b = grouped ? (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH_GROUPED
+                                                      : F110QP_LANE_MIN_BATCH_GROUPED_WIDE)
+                              : (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH : F110QP_LANE_MIN_BATCH_WIDE);
+    be = (!gap && batch >= min_b) ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
+  }
+  if (gap) be = F110QP_BACKEND_WAVE;
+  f110qp::LaneWork lw;
+  lw.mode = c->lane_mode;
+  lw.qpw = c->lane_qpw;
+  const bool lane = be == F110QP_BACKEND_LANE;
+  if (backend) *backend = be;
+  if (qps_per_wave) *qps_per_wave = lane ? f110qp::lane_qps_per_wave(batch, lw.qpw) : 1;
+  if (scratch) *scratch = lane ? f110qp::lane_scratch_mode(c->kp, batch, lw) : 0;
+  return F110QP_OK;
+}
+
+int f110qp_select_dev(int batch, const int* group, int num_groups, const double* cost,
+                      const int* status, int* winner, double* best_cost, void* stream) {
+  if (batch < 0 || num_groups < 0) return fail(F110QP_ERR_INVALID, "batch / num_groups < 0");
+  if (num_groups == 0) return F110QP_OK;
+  if (!winner || !best_cost || (batch > 0 && (!group || !cost || !status)))
+    return fail(F110QP_ERR_INVALID, "NULL pointer argument");
+  hipError_t e = f110qp::launch_select(batch, group, num_groups, cost, status, winner, best_cost,
+                                       (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "select kernel launch");
+  return F110QP_OK;
 }
 
 }  // extern "C"
 
 static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul, const float* xr,
                       const float* hs, const int* group, int num_groups, float* uo, float* xo,
-                      int* st, int* it) {
+                      int* st, int* it, double* obj, double* cost) {
   int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
   if (rc || batch == 0) return rc;
   hipError_t e = hipSetDevice(c->cfg.device);
@@ -384,9 +452,12 @@ static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul
   const size_t s_x0 = B * 3 * 4, s_ul = B * 2 * 4, s_xr = B * S * 3 * 4, s_hs = B * 6 * 4;
   const size_t s_uo = B * N * 2 * 4, s_xo = B * (N + 1) * 3 * 4, s_st = B * 4;
   // packed layouts (every size a multiple of 4 bytes): in = x0 | u_lin | x_ref | halfspace,
-  // out = u | x | status | iters
+  // out = u | x | status | iters | obj | cost (the doubles 8-byte aligned)
   const size_t o_ul = s_x0, o_xr = o_ul + s_ul, o_hs = o_xr + s_xr, in_bytes = o_hs + (gap ? s_hs : 0);
-  const size_t o_xo = s_uo, o_st = o_xo + s_xo, o_it = o_st + s_st, out_bytes = o_it + s_st;
+  const size_t o_xo = s_uo, o_st = o_xo + s_xo, o_it = o_st + s_st;
+  const size_t o_ob = (o_it + s_st + 7) & ~(size_t)7, s_ob = B * 8;
+  const size_t o_co = o_ob + (obj ? s_ob : 0);
+  const size_t out_bytes = o_co + (cost ? s_ob : 0);
   if ((e = c->hin.ensure(in_bytes)) || (e = c->hout.ensure(out_bytes)))
     return hip_fail(e, "hipHostMalloc staging");
   char* hi = (char*)c->hin.p;
@@ -408,6 +479,9 @@ static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul
   }
   int backend;
   f110qp::LaneWork lw;
+  f110qp::ObjOut oo;
+  oo.obj = obj ? (double*)(dq + o_ob) : nullptr;
+  oo.cost = cost ? (double*)(dq + o_co) : nullptr;
   if (group) {
     if ((e = c->dgrp.ensure(B * 4)) || (e = hipMemcpyAsync(c->dgrp.p, group, B * 4, hipMemcpyHostToDevice, s)))
       return hip_fail(e, "group ids H2D");
@@ -418,7 +492,7 @@ static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul
     e = f110qp::launch_solve_grouped(c->kp, batch, (const float*)di, (const float*)(di + o_ul),
                                      (const float*)(di + o_xr), gap ? (const float*)(di + o_hs) : nullptr,
                                      (float*)dq, (float*)(dq + o_xo), (int*)(dq + o_st),
-                                     (int*)(dq + o_it), gws, leader, backend, lw, s);
+                                     (int*)(dq + o_it), gws, leader, backend, lw, oo, s);
   } else {
     f110qp::WarmState ws;
     if ((rc = warm_state(c, batch, s, &ws))) return rc;
@@ -426,7 +500,7 @@ static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul
     e = f110qp::launch_solve(c->kp, batch, (const float*)di, (const float*)(di + o_ul),
                              (const float*)(di + o_xr), gap ? (const float*)(di + o_hs) : nullptr,
                              (float*)dq, (float*)(dq + o_xo), (int*)(dq + o_st), (int*)(dq + o_it),
-                             ws, backend, lw, s);
+                             ws, backend, lw, oo, s);
   }
   if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
   if (!zc && (e = hipMemcpyAsync(c->hout.p, dq, out_bytes, hipMemcpyDeviceToHost, s)))
@@ -438,6 +512,8 @@ static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul
   std::memcpy(xo, ho + o_xo, s_xo);
   std::memcpy(st, ho + o_st, s_st);
   if (it) std::memcpy(it, ho + o_it, s_st);
+  if (obj) std::memcpy(obj, ho + o_ob, s_ob);
+  if (cost) std::memcpy(cost, ho + o_co, s_ob);
   return F110QP_OK;
 }
 

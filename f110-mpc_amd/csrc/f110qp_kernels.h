@@ -55,9 +55,20 @@ struct LaneWork {
   int dref = 1;   // 1: fp64 references in LDS when the resident waves fit (DREF); 0: float
 };
 
+// Optional per-QP objective outputs (fp64, computed in the kernels' output sweeps from the fp64
+// solution): obj[b] = OSQP's objective 1/2 z'Pz + q'z of the reference QP (mpc.cpp:208-229;
+// OSQP drops the constant), cost[b] = the same plus that constant
+// 1/2 sum_i r_i'Q r_i + N/2 u_des'R u_des, i.e. sum 1/2|x_i - r_i|_Q^2 + 1/2|u_i - u_des|_R^2 >= 0.
+struct ObjOut {
+  double* obj = nullptr;
+  double* cost = nullptr;
+};
+
 // waves the lane kernel's grid aims for (one per CU of the MI355X's 256)
 constexpr int kLaneTargetWaves = 256;
 int lane_qps_per_wave(int B, int qpw);
+// scratch placement the lane launch picks for a batch: 1 LDS fp64, 2 LDS fp32, 3 HBM fp64, 4 HBM fp32
+int lane_scratch_mode(const KParams& P, int B, const LaneWork& lw);
 
 enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
 
@@ -66,12 +77,13 @@ enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u_lin,
                         const float* x_ref, const float* hs, float* u_out, float* x_out,
                         int* status, int* iters, const WarmState& warm, int backend,
-                        const LaneWork& lw, hipStream_t stream);
+                        const LaneWork& lw, const ObjOut& oo, hipStream_t stream);
 
 // The lane-per-QP kernel alone (box rows).
 hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* u_lin,
                        const float* x_ref, float* u_out, float* x_out, int* status, int* iters,
-                       const WarmState& warm, const LaneWork& lw, hipStream_t stream);
+                       const WarmState& warm, const LaneWork& lw, const ObjOut& oo,
+                       hipStream_t stream);
 
 // Grouped solve: leader (smallest member) of every group, W = H^-1 per group from its leader,
 // then the solve (wave back end; the lane back end has no factor to share and ignores groups).
@@ -79,7 +91,14 @@ hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* u_
 hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const float* u_lin,
                                 const float* x_ref, const float* hs, float* u_out, float* x_out,
                                 int* status, int* iters, const WarmState& gws, int* leader,
-                                int backend, const LaneWork& lw, hipStream_t stream);
+                                int backend, const LaneWork& lw, const ObjOut& oo,
+                                hipStream_t stream);
+
+// Per-scenario selection (the argmin of src/project.cpp:125-136 taken over the
+// QP costs): winner[g] = the smallest b with group[b] == g, status[b] == SOLVED and the minimal
+// cost[b]; -1 when the group has no solved member. best[g] = that cost (+inf if none).
+hipError_t launch_select(int B, const int* group, int G, const double* cost, const int* status,
+                         int* winner, double* best, hipStream_t stream);
 
 // Dump the condensed H (B x 2N x 2N) and g (B x 2N) as built by the solve kernel.
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* u_lin,

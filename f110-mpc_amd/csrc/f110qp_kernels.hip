@@ -13,7 +13,7 @@ template <int NUM, bool GAP>
 hipError_t launch_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                     const float* hs, float* uo, float* xo, int* st, int* its, double* Hd,
                     double* gd, const WarmState& ws, const int* list, const int* count, int grid,
-                    hipStream_t s);  // solve_inst.hip
+                    const ObjOut& oo, hipStream_t s);  // solve_inst.hip
 template <int NUM, bool GAP>
 hipError_t launch_prep_t(const KParams& P, int B, const float* x0, const float* ul,
                          const float* xr, const float* hs, const WarmState& ws, const int* leader,
@@ -23,12 +23,12 @@ template <bool GAP>
 static hipError_t launch_g(const KParams& P, int B, const float* x0, const float* ul,
                            const float* xr, const float* hs, float* uo, float* xo, int* st,
                            int* its, double* Hd, double* gd, const WarmState& ws, const int* list,
-                           const int* count, int grid, hipStream_t s) {
+                           const int* count, int grid, const ObjOut& oo, hipStream_t s) {
   const int NU = 2 * P.N;
 #define F110QP_CASE(NUM)                                                                    \
   if (NU <= NUM)                                                                            \
     return launch_t<NUM, GAP>(P, B, x0, ul, xr, hs, uo, xo, st, its, Hd, gd, ws, list, count, \
-                              grid, s);
+                              grid, oo, s);
   F110QP_CASE(8) F110QP_CASE(16) F110QP_CASE(24) F110QP_CASE(32) F110QP_CASE(40)
   F110QP_CASE(48) F110QP_CASE(56) F110QP_CASE(64) F110QP_CASE(80) F110QP_CASE(96)
 #undef F110QP_CASE
@@ -38,14 +38,14 @@ static hipError_t launch_g(const KParams& P, int B, const float* x0, const float
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
                         const float* xr, const float* hs, float* uo, float* xo, int* st,
                         int* its, const WarmState& ws, int backend, const LaneWork& lw,
-                        hipStream_t s) {
+                        const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (hs)
     return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
-                          nullptr, B, s);
-  if (backend == BACKEND_LANE) return launch_lane(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+                          nullptr, B, oo, s);
+  if (backend == BACKEND_LANE) return launch_lane(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
   return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
-                         nullptr, B, s);
+                         nullptr, B, oo, s);
 }
 
 template <bool GAP>
@@ -74,10 +74,10 @@ __global__ __launch_bounds__(256) void group_mark_kernel(const int B, const int*
 hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const float* ul,
                                 const float* xr, const float* hs, float* uo, float* xo, int* st,
                                 int* its, const WarmState& gws, int* leader, int backend,
-                                const LaneWork& lw, hipStream_t s) {
+                                const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   if (!hs && backend == BACKEND_LANE)  // per-QP Riccati: nothing to share
-    return launch_solve(P, B, x0, ul, xr, hs, uo, xo, st, its, WarmState(), backend, lw, s);
+    return launch_solve(P, B, x0, ul, xr, hs, uo, xo, st, its, WarmState(), backend, lw, oo, s);
   hipError_t e = hipMemsetAsync(leader, 0x7f, (size_t)gws.ngroups * sizeof(int), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(group_mark_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, gws.group,
@@ -87,16 +87,89 @@ hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const 
          : launch_prep_g<false>(P, B, x0, ul, xr, hs, gws, leader, s);
   if (e != hipSuccess) return e;
   return hs ? launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, gws, nullptr,
-                             nullptr, B, s)
+                             nullptr, B, oo, s)
             : launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, gws,
-                              nullptr, nullptr, B, s);
+                              nullptr, nullptr, B, oo, s);
 }
 
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* ul,
                                  const float* xr, double* Hd, double* gd, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   return launch_g<false>(P, B, x0, ul, xr, nullptr, nullptr, nullptr, nullptr, nullptr, Hd, gd,
-                         WarmState(), nullptr, nullptr, B, s);
+                         WarmState(), nullptr, nullptr, B, ObjOut(), s);
+}
+
+// ---- per-scenario selection (f110qp_select_dev) --------------------------------------------
+// Two passes of 64-bit atomics over one grid-stride launch each: (1) the group minimum of the
+// solved members' cost bits (a non-negative double orders like its bit pattern), (2) the smallest
+// member index attaining it. Exact (no rounding of the cost into a packed key) and
+// deterministic; O(B) with one atomic per QP and pass.
+__global__ __launch_bounds__(256) void select_init_kernel(int G, unsigned long long* __restrict__ bits,
+                                                          int* __restrict__ winner) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g < G) {
+    bits[g] = 0x7ff0000000000000ull;  // +inf: no solved member yet
+    winner[g] = 0x7fffffff;
+  }
+}
+
+__device__ __forceinline__ bool select_eligible(int b, const int* group, int G, const double* cost,
+                                                const int* status, int* gout, unsigned long long* cb) {
+  const int g = group[b];
+  const double c = cost[b];
+  if (g < 0 || g >= G || status[b] != F110QP_SOLVED_ID || !(c >= 0.0) || !(c < 1.0e308)) return false;
+  *gout = g;
+  *cb = (unsigned long long)__double_as_longlong(c + 0.0);  // -0.0 -> +0.0
+  return true;
+}
+
+__global__ __launch_bounds__(256) void select_min_kernel(int B, const int* __restrict__ group, int G,
+                                                         const double* __restrict__ cost,
+                                                         const int* __restrict__ status,
+                                                         unsigned long long* __restrict__ bits) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  int g;
+  unsigned long long cb;
+  if (b < B && select_eligible(b, group, G, cost, status, &g, &cb)) atomicMin(bits + g, cb);
+}
+
+__global__ __launch_bounds__(256) void select_arg_kernel(int B, const int* __restrict__ group, int G,
+                                                         const double* __restrict__ cost,
+                                                         const int* __restrict__ status,
+                                                         const unsigned long long* __restrict__ bits,
+                                                         int* __restrict__ winner) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  int g;
+  unsigned long long cb;
+  if (b < B && select_eligible(b, group, G, cost, status, &g, &cb) && cb == bits[g])
+    atomicMin(winner + g, b);
+}
+
+__global__ __launch_bounds__(256) void select_fin_kernel(int G, const unsigned long long* __restrict__ bits,
+                                                         int* __restrict__ winner, double* __restrict__ best) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g < G) {
+    const bool none = winner[g] == 0x7fffffff;
+    if (none) winner[g] = -1;
+    // best aliases bits (same 8-byte slots): the value is read before it is overwritten
+    const double v = __longlong_as_double((long long)bits[g]);
+    if (best) best[g] = v;
+  }
+}
+
+hipError_t launch_select(int B, const int* group, int G, const double* cost, const int* status,
+                         int* winner, double* best, hipStream_t s) {
+  if (G <= 0) return hipSuccess;
+  // the minimum bits live in `best` (G doubles, caller-provided) and become the best cost
+  unsigned long long* bits = reinterpret_cast<unsigned long long*>(best);
+  hipLaunchKernelGGL(select_init_kernel, dim3((G + 255) / 256), dim3(256), 0, s, G, bits, winner);
+  if (B > 0) {
+    hipLaunchKernelGGL(select_min_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, group, G, cost, status, bits);
+    hipLaunchKernelGGL(select_arg_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, group, G, cost, status, bits,
+                       winner);
+  }
+  hipLaunchKernelGGL(select_fin_kernel, dim3((G + 255) / 256), dim3(256), 0, s, G, bits, winner, best);
+  return hipGetLastError();
 }
 
 }  // namespace f110qp

@@ -18,7 +18,8 @@
 // finds run starts with shifts of the ballot (the carry of block k-1's top beam included) and
 // the start of each lane's run as the highest start bit at or below it (or the last start of an
 // earlier block, a wave-uniform scalar). Each lane keeps the best key (p - s) << 16 | (65535 - p)
-// (larger run first, then the earlier beam); one wave max-reduction ends the scan. Lane 0 then
+// as an UNSIGNED 32-bit value (p - s <= 65534, so the key never overflows; 0 = no run) (larger
+// run first, then the earlier beam); one wave max-reduction ends the scan. Lane 0 then
 // evaluates the endpoints and the two half-spaces with the reference's float/double types.
 // FP contraction is off for the whole kernel body (hipcc fuses a*b+c into an FMA by default and
 // does so even through the __fmul_rn/__fadd_rn helpers, which are plain operators inlined from
@@ -35,9 +36,9 @@ namespace f110qp {
 constexpr int kHsWaves = 4;   // scans (waves) per 256-thread workgroup
 constexpr int kHsBatch = 24;  // 64-beam blocks loaded per lane before they are consumed (1,536 beams)
 
-__device__ __forceinline__ int wave_max_i32(int v) {
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
   return v;
 }
 
@@ -60,12 +61,14 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   if (num_scans > nr) num_scans = nr;
   const float lim = 1.571f / divider;  // :135
   const int nblk = num_scans > 0 ? (num_scans + 63) / 64 : 0;
-  int best = -1;              // per-lane best key
+  unsigned best = 0u;         // per-lane best key (0: no run of >= 2 beams)
   int last_start = -1;        // last run start in the blocks before k (wave-uniform)
   bool top_open = false;      // beam 64 k - 1 open (wave-uniform)
   int w0 = -1;                // first in-window beam (wave-uniform)
   bool w0_open = false;
   float v[kHsBatch];  // the last batch of blocks stays in registers for the tail
+#pragma unroll
+  for (int j = 0; j < kHsBatch; j++) v[j] = 0.f;
   for (int k0 = 0; k0 < nblk; k0 += kHsBatch) {
 #pragma unroll
     for (int j = 0; j < kHsBatch; j++) {  // unconditional loads (clamped index): no exec masking
@@ -91,18 +94,18 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
       const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
       const unsigned long long Sb = S & upto;
       const int s = Sb ? 64 * k + 63 - __builtin_clzll(Sb) : last_start;
-      if (open && s < p) best = max(best, ((p - s) << 16) | (65535 - p));
+      if (open && s < p) best = max(best, ((unsigned)(p - s) << 16) | (unsigned)(65535 - p));
       if (S) last_start = 64 * k + 63 - __builtin_clzll(S);
       top_open = (M >> 63) & 1ull;
     }
   }
-  best = wave_max_i32(best);
+  best = wave_max_u32(best);
   // The tail runs on every lane with the same values (a partially masked wave runs ~2.4x slower
   // on a loaded CU, tools/microbench/contention.hip); lane 0 stores.
   int best_lo, best_hi;
-  if (best >= 0) {
-    best_hi = 65535 - (best & 0xffff);
-    best_lo = best_hi - (best >> 16);
+  if (best != 0u) {
+    best_hi = 65535 - (int)(best & 0xffffu);
+    best_lo = best_hi - (int)(best >> 16);
   } else if (w0 >= 0 && !w0_open) {
     best_lo = best_hi = -1;  // the initial (lo, hi) recorded on the window's first (short) beam
   } else {
@@ -131,9 +134,10 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   const double s1 = __shfl(sl, 0), c1d = __shfl(cl, 0);
   const double s2 = __shfl(sl, 1), c2d = __shfl(cl, 1);
   // ranges[best_lo], ranges[best_hi]: from the registers of the last batch when the scan fits
-  // one batch (1,536 beams), else re-read (L2)
+  // one batch (1,536 beams), else re-read (L2). An empty window (num_scans <= 0: no block was
+  // loaded, (lo, hi) = (0, 0)) reads ranges[0] as the reference does.
   float rlo, rhi;
-  if (nblk <= kHsBatch) {
+  if (nblk >= 1 && nblk <= kHsBatch) {
     const int klo = best_lo >> 6, khi = best_hi >> 6;
     float vlo = 0.f, vhi = 0.f;
 #pragma unroll

@@ -17,7 +17,7 @@ namespace f110qp {
 #define F110QP_INST_R(ST, SLDS, ROT, DREF)                                                     \
   template hipError_t launch_lane_t<ST, SLDS, F110QP_LQ, ROT, DREF>(                           \
       const KParams&, int, const float*, const float*, const float*, float*, float*, int*, int*, \
-      const WarmState&, const LaneWork&, size_t, hipStream_t);
+      const WarmState&, const LaneWork&, const ObjOut&, size_t, hipStream_t);
 F110QP_INST(double, true)
 F110QP_INST(float, true)
 F110QP_INST(float, false)

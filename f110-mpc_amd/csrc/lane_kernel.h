@@ -112,7 +112,8 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
                                                   int* __restrict__ status_out,
                                                   int* __restrict__ iters_out,
                                                   double* __restrict__ scr,
-                                                  const WarmState ws, const int kmax) {
+                                                  const WarmState ws, const int kmax,
+                                                  const ObjOut oo) {
   extern __shared__ __attribute__((aligned(16))) float xr_s[];  // [3N][L] x_ref, transposed
   // DREF: the references are kept as recentred (and, ROT, rotated) fp64 offsets [3N][L] at the
   // start of LDS, converted once after staging; the float staging then sits in the upper half
@@ -206,6 +207,23 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
   const double ud0 = P.udes[0], ud1 = P.udes[1];
   const double lb0 = (double)P.umin[0], lb1 = (double)P.umin[1];
   const double ub0 = (double)P.umax[0], ub1 = (double)P.umax[1];
+  // PDAS flip tolerances (scaled): a free input enters its bound only when it is outside by more
+  // than ptol, a fixed one leaves only when its multiplier is below -gtol, so that a degenerate
+  // bound (zero multiplier: u_des on a bound and the reference tracked exactly) cannot flip free ->
+  // bound -> free on rounding noise. fp64 gains: 1e-10 (noise ~1e-15), every pass. fp32 gains
+  // (u carry ~1e-7 relative noise): exact compares in the PDAS passes (the accuracy of round 2),
+  // 1e-6 / 1e-5 in the single-flip passes after kmax, where a degenerate QP then settles (its
+  // KKT point exact to ~ptol, well inside the 1e-4 parity bound).
+  constexpr bool F32 = sizeof(ST) == 4;
+  constexpr double kPtT = F32 ? 0.0 : 1e-10, kGtT = F32 ? 0.0 : 1e-10;  // PDAS passes
+  constexpr double kPtL = F32 ? 1e-6 : 1e-10, kGtL = F32 ? 1e-5 : 1e-10;  // single-flip passes
+  auto tols = [&](bool loose, double& l0, double& u0, double& l1, double& u1, double& g0, double& g1) {
+    const double pt = loose ? kPtL : kPtT, gt = loose ? kGtL : kGtT;
+    l0 = lb0 - pt * (1.0 + fabs(lb0)); u0 = ub0 + pt * (1.0 + fabs(ub0));
+    l1 = lb1 - pt * (1.0 + fabs(lb1)); u1 = ub1 + pt * (1.0 + fabs(ub1));
+    g0 = gt * (1.0 + r0 * (1.0 + fabs(lb0) + fabs(ub0)));
+    g1 = gt * (1.0 + r1 * (1.0 + fabs(lb1) + fabs(ub1)));
+  };
 
   // scratch slot (i, e) of this QP: sp[8 L i + e ES] (LDS [stage][8][L]: ES = L; HBM
   // [stage][L][8]: ES = 1); the PDAS state of stage i (2 bits
@@ -406,6 +424,8 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
         // box.)
         auto forward = [&](auto mode_tag) -> bool {
         constexpr int MODE = decltype(mode_tag)::value;
+        double lbe0, ube0, lbe1, ube1, gtol0, gtol1;
+        tols(MODE == 1, lbe0, ube0, lbe1, ube1, gtol0, gtol1);
         bool changed = false;
         bool flipped = false;  // single-flip passes: the first violation of this sweep is taken
         {
@@ -458,13 +478,15 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
                 for (int a = 0; a < 2; a++) {
                   const int ca = (old >> (2 * a)) & 3;
                   const double u = a ? u1 : u0, g = a ? g1 : g0;
-                  const double lb = a ? lb1 : lb0, ub = a ? ub1 : ub0;
                   // a fixed input sits exactly on its bound (k carries the bound, its K row is
                   // zero), so the HIK test reduces to the multiplier's sign for a fixed input and
-                  // to the bound test for a free one
+                  // to the bound test for a free one — both with a small tolerance, so that a
+                  // degenerate bound (zero multiplier, e.g. u_des on a bound and the reference
+                  // tracked exactly) cannot flip free -> bound -> free on rounding noise
                   // (bitwise, every compare evaluated: no EXEC-masked region per input and stage)
-                  const bool nlo = ((ca == 1) & (g > 0.0)) | ((ca == 0) & (u < lb));
-                  const bool nhi = !nlo & (((ca == 2) & (g < 0.0)) | ((ca == 0) & (u > ub)));
+                  const double gt = a ? gtol1 : gtol0;
+                  const bool nlo = ((ca == 1) & (g > -gt)) | ((ca == 0) & (u < (a ? lbe1 : lbe0)));
+                  const bool nhi = !nlo & (((ca == 2) & (g < gt)) | ((ca == 0) & (u > (a ? ube1 : ube0))));
                   const int nca = (int)nlo | ((int)nhi << 1);
                   if constexpr (MODE == 0) {
                     st |= nca << (2 * a);
@@ -489,6 +511,8 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
         changed = single ? forward(ModeTag<1>{}) : forward(ModeTag<0>{});
       } else {
         bool flipped = false;  // single-flip passes: the first violation of this sweep is taken
+        double lbe0, ube0, lbe1, ube1, gtol0, gtol1;
+        tols(single, lbe0, ube0, lbe1, ube1, gtol0, gtol1);
         {
           double x0 = 0.0, x1 = 0.0, x2 = 0.0;  // recentred x_0
           double l0 = p0, l1 = p1, l2 = p2;      // lambda_0 = P_0 x_0 + p_0 = p_0
@@ -539,13 +563,15 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
                 for (int a = 0; a < 2; a++) {
                   const int ca = (old >> (2 * a)) & 3;
                   const double u = a ? u1 : u0, g = a ? g1 : g0;
-                  const double lb = a ? lb1 : lb0, ub = a ? ub1 : ub0;
                   // a fixed input sits exactly on its bound (k carries the bound, its K row is
                   // zero), so the HIK test reduces to the multiplier's sign for a fixed input and
-                  // to the bound test for a free one
+                  // to the bound test for a free one — both with a small tolerance, so that a
+                  // degenerate bound (zero multiplier, e.g. u_des on a bound and the reference
+                  // tracked exactly) cannot flip free -> bound -> free on rounding noise
                   // (bitwise, every compare evaluated: no EXEC-masked region per input and stage)
-                  const bool nlo = ((ca == 1) & (g > 0.0)) | ((ca == 0) & (u < lb));
-                  const bool nhi = !nlo & (((ca == 2) & (g < 0.0)) | ((ca == 0) & (u > ub)));
+                  const double gt = a ? gtol1 : gtol0;
+                  const bool nlo = ((ca == 1) & (g > -gt)) | ((ca == 0) & (u < (a ? lbe1 : lbe0)));
+                  const bool nhi = !nlo & (((ca == 2) & (g < gt)) | ((ca == 0) & (u > (a ? ube1 : ube0))));
                   const int nca = (int)nlo | ((int)nhi << 1);
                   const bool take = (nca != ca) & !(single & flipped);
                   st = take ? ((st & ~(3 << (2 * a))) | (nca << (2 * a))) : st;
@@ -629,6 +655,41 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
     }
   }
   LACC(acc_out, t_out);
+  if (oo.obj || oo.cost) {
+    // objective of the solution (fp64): cost = sum_{i=0..N} 1/2|x_i - r_i|_Q^2 + sum 1/2|u_i - u_des|_R^2
+    // (r_N = x_ref[N-1], mpc.cpp:228) by one more rollout from the final gains, and OSQP's
+    // 1/2 z'Pz + q'z = cost - 1/2 sum r_i'Q r_i - N/2 u_des'R u_des (world coordinates). In the
+    // heading frame Q = diag(q0, q0, q2) is rotation invariant, so the tracking term is taken there.
+    const bool solved = done && !bad;
+    double x0 = 0.0, x1 = 0.0, x2 = 0.0, J = 0.0, Cr = 0.0;
+    auto qterm = [&](int i, double e0, double e1, double e2) {
+      double rx, ry, rt;
+      ref(i, rx, ry, rt);
+      const double d0 = e0 - rx, d1 = e1 - ry, d2 = e2 - rt;
+      J += 0.5 * (q0 * d0 * d0 + q1 * d1 * d1 + q2 * d2 * d2);
+      const double wx = (ROT ? cs * rx - sn * ry : rx) + X0, wy = (ROT ? sn * rx + cs * ry : ry) + Y0;
+      const double wt = rt + th0;
+      Cr += 0.5 * (q0 * wx * wx + q1 * wy * wy + q2 * wt * wt);
+    };
+    qterm(0, 0.0, 0.0, 0.0);
+    for (int i = 0; i < N; i++) {
+      const ST* s = sp + (size_t)i * 8 * L;
+      const double K00 = s[0], K01 = s[ES], K02 = s[2 * ES], K10 = s[3 * ES];
+      const double K11 = s[4 * ES], K12 = s[5 * ES], k0 = s[6 * ES], k1 = s[7 * ES];
+      const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
+      const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
+      J += 0.5 * (r0 * (u0 - ud0) * (u0 - ud0) + r1 * (u1 - ud1) * (u1 - ud1));
+      const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
+      const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;
+      const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
+      x0 = nx0; x1 = nx1; x2 = nx2;
+      qterm(i + 1 < N ? i + 1 : N - 1, x0, x1, x2);
+    }
+    const double Cu = 0.5 * (double)N * (r0 * ud0 * ud0 + r1 * ud1 * ud1);
+    const double nanv = __longlong_as_double(0x7ff8000000000000ll);
+    if (owner && oo.cost) oo.cost[b] = solved ? J : nanv;
+    if (owner && oo.obj) oo.obj[b] = solved ? J - Cr - Cu : nanv;
+  }
   if (owner && ws.act) {  // active set of this solution for the next tick
     unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
     for (int i = 0; i < N; i++) {
@@ -667,7 +728,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
 template <typename ST, bool SLDS, int L, bool ROT, bool DREF>
 hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                          float* uo, float* xo, int* st, int* its, const WarmState& ws,
-                         const LaneWork& lw, size_t lds, hipStream_t s) {
+                         const LaneWork& lw, const ObjOut& oo, size_t lds, hipStream_t s) {
   const int waves = (B + L - 1) / L;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_kernel<ST, SLDS, L, ROT, DREF>),
@@ -675,7 +736,7 @@ hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* 
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL((lane_kernel<ST, SLDS, L, ROT, DREF>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr,
-                     uo, xo, st, its, lw.scratch, ws, lw.kmax);
+                     uo, xo, st, its, lw.scratch, ws, lw.kmax, oo);
   return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ namespace f110qp {
 template <typename ST, bool SLDS, int L, bool ROT, bool DREF>
 hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                          float* uo, float* xo, int* st, int* its, const WarmState& ws,
-                         const LaneWork& lw, size_t lds, hipStream_t s);  // lane_inst.hip
+                         const LaneWork& lw, const ObjOut& oo, size_t lds, hipStream_t s);  // lane_inst.hip
 #endif
 
 // QPs per wave: the smallest power of two (<= 64) that fits the batch in kLaneTargetWaves waves
@@ -34,48 +34,62 @@ int lane_qps_per_wave(int B, int qpw) {
 template <typename ST, bool SLDS, int L, bool DREF>
 static hipError_t launch_rot_d(const KParams& P, int B, const float* x0, const float* ul,
                                const float* xr, float* uo, float* xo, int* st, int* its,
-                               const WarmState& ws, const LaneWork& lw, size_t lds, hipStream_t s) {
+                               const WarmState& ws, const LaneWork& lw, const ObjOut& oo, size_t lds,
+                               hipStream_t s) {
   if (lw.rot && P.q[0] == P.q[1])
-    return launch_lane_t<ST, SLDS, L, true, DREF>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
-  return launch_lane_t<ST, SLDS, L, false, DREF>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
+    return launch_lane_t<ST, SLDS, L, true, DREF>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, lds, s);
+  return launch_lane_t<ST, SLDS, L, false, DREF>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, lds, s);
 }
 template <typename ST, bool SLDS, int L>
 static hipError_t launch_rot(const KParams& P, int B, const float* x0, const float* ul,
                              const float* xr, float* uo, float* xo, int* st, int* its,
-                             const WarmState& ws, const LaneWork& lw, size_t lds, hipStream_t s) {
+                             const WarmState& ws, const LaneWork& lw, const ObjOut& oo, size_t lds,
+                             hipStream_t s) {
   const size_t ldsd = lds + (size_t)P.N * L * 12;
   const size_t per_cu = (((size_t)B + L - 1) / L + 255) / 256;
   if (lw.dref && per_cu == 1 && ldsd <= 160 * 1024)
-    return launch_rot_d<ST, SLDS, L, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, ldsd, s);
-  return launch_rot_d<ST, SLDS, L, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds, s);
+    return launch_rot_d<ST, SLDS, L, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, ldsd, s);
+  return launch_rot_d<ST, SLDS, L, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, lds, s);
 }
 
-template <int L>
-static hipError_t launch_lq(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
-                            float* uo, float* xo, int* st, int* its, const WarmState& ws,
-                            const LaneWork& lw, hipStream_t s) {
+// Scratch placement of the lane kernel for a batch (lane_mode 0 = auto; 1/2/3/4 force LDS fp64 /
+// LDS fp32 / HBM fp64 / HBM fp32): auto puts the scratch in LDS when every wave of the grid is
+// resident with it (waves per CU x its LDS within the CU's 160 KiB): fp64 if that fits, else
+// fp32; otherwise fp32 in the HBM workspace (the waves then stay resident on the 16 N L bytes of
+// references + state alone). With the state recentred on x0 the fp32 gains and trajectories stay
+// within ~1e-7 of the exact optimum (tests/test_gpu_parity.py::test_lane_backend_scratch_modes).
+static int scratch_mode(const KParams& P, int B, int L, int mode) {
   const size_t N = (size_t)P.N;
   const size_t base = N * L * (12 + 4);  // references + PDAS state
   const size_t lds64 = base + N * 8 * L * sizeof(double), lds32 = base + N * 8 * L * sizeof(float);
   const size_t cap = 160 * 1024;
-  int mode = lw.mode;
-  // auto: the scratch in LDS when every wave of the grid is resident with it (waves per CU x
-  // its LDS within the CU's 160 KiB): fp64 if that fits, else fp32; otherwise fp32 in the HBM
-  // workspace (the waves then stay resident on the 16 N L bytes of references + state alone).
-  // With the state recentred on x0 the fp32 gains and trajectories stay within ~1e-7 of the
-  // exact optimum (tests/test_gpu_parity.py::test_lane_backend_scratch_modes).
   if (mode == 0) {
     const size_t waves = ((size_t)B + L - 1) / L;
     const size_t per_cu = (waves + 255) / 256;
     mode = per_cu * lds64 <= cap ? 1 : per_cu * lds32 <= cap ? 2 : 4;
   }
-  if (mode == 1 && lds64 <= cap)
-    return launch_rot<double, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds64, s);
-  if (mode == 2 && lds32 <= cap)
-    return launch_rot<float, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, lds32, s);
-  if (mode == 4 || mode == 2)
-    return launch_rot<float, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
-  return launch_rot<double, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, base, s);
+  if (mode == 1 && lds64 > cap) mode = 3;
+  if (mode == 2 && lds32 > cap) mode = 4;
+  return mode;
+}
+
+int lane_scratch_mode(const KParams& P, int B, const LaneWork& lw) {
+  return scratch_mode(P, B, lane_qps_per_wave(B, lw.qpw), lw.mode);
+}
+
+template <int L>
+static hipError_t launch_lq(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
+                            float* uo, float* xo, int* st, int* its, const WarmState& ws,
+                            const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
+  const size_t N = (size_t)P.N;
+  const size_t base = N * L * (12 + 4);
+  const size_t lds64 = base + N * 8 * L * sizeof(double), lds32 = base + N * 8 * L * sizeof(float);
+  switch (scratch_mode(P, B, L, lw.mode)) {
+    case 1: return launch_rot<double, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, lds64, s);
+    case 2: return launch_rot<float, true, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, lds32, s);
+    case 3: return launch_rot<double, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, base, s);
+    default: return launch_rot<float, false, L>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, base, s);
+  }
 }
 
 // LDS per wave: the staged references (12 N L B) + PDAS state (4 N L B) + Riccati scratch
@@ -83,16 +97,16 @@ static hipError_t launch_lq(const KParams& P, int B, const float* x0, const floa
 // fp32).
 hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* ul,
                        const float* xr, float* uo, float* xo, int* st, int* its,
-                       const WarmState& ws, const LaneWork& lw, hipStream_t s) {
+                       const WarmState& ws, const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   switch (lane_qps_per_wave(B, lw.qpw)) {
-    case 1: return launch_lq<1>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
-    case 2: return launch_lq<2>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
-    case 4: return launch_lq<4>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
-    case 8: return launch_lq<8>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
-    case 16: return launch_lq<16>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
-    case 32: return launch_lq<32>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
-    default: return launch_lq<64>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, s);
+    case 1: return launch_lq<1>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    case 2: return launch_lq<2>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    case 4: return launch_lq<4>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    case 8: return launch_lq<8>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    case 16: return launch_lq<16>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    case 32: return launch_lq<32>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    default: return launch_lq<64>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
   }
 }
 

@@ -9,7 +9,7 @@
   template hipError_t f110qp::launch_t<NUM, GAP>(                                              \
       const KParams&, int, const float*, const float*, const float*, const float*, float*,      \
       float*, int*, int*, double*, double*, const WarmState&, const int*, const int*, int,       \
-      hipStream_t);                                                                            \
+      const ObjOut&, hipStream_t);                                                             \
   template hipError_t f110qp::launch_prep_t<NUM, GAP>(const KParams&, int, const float*,       \
                                                       const float*, const float*, const float*,  \
                                                       const WarmState&, const int*, hipStream_t);

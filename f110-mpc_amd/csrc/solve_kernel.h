@@ -716,7 +716,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
                                          int* __restrict__ iters_out,
                                          double* __restrict__ Hdbg,
                                          double* __restrict__ gdbg,
-                                         const WarmState& ws, const int prep_slot = -1) {
+                                         const WarmState& ws, const ObjOut& oo,
+                                         const int prep_slot = -1) {
   constexpr int R = (NUM + 63) / 64;
   const int lane = threadIdx.x;
   const int N = P.N;
@@ -1560,6 +1561,41 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         xo[3 * (kk[r] + 1) + 2] = ok ? (float)th[r] : nanv;
       }
     }
+    if (oo.obj || oo.cost) {
+      // objective (fp64): cost = sum_{i=0..N} 1/2|x_i - r_i|_Q^2 + sum 1/2|u - u_des|_R^2 (r_N =
+      // x_ref[N-1], mpc.cpp:228; odd lanes hold stage kk+1, lane 0 stage 0), and OSQP's
+      // 1/2 z'Pz + q'z = cost - 1/2 sum r_i'Q r_i - N/2 u_des'R u_des (world coordinates)
+      const double q0 = P.q[0], q1 = P.q[1], q2 = P.q[2];
+      double J = 0.0, Cr = 0.0;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (!valid[r]) continue;
+        const double ra = a ? P.r[1] : P.r[0], uda = a ? P.udes[1] : P.udes[0];
+        J += 0.5 * ra * (uo[r] - uda) * (uo[r] - uda);
+        if (a == 1) {
+          const double dx = px[r] - sm.rx[vv[r]], dy = py[r] - sm.ry[vv[r]];
+          const double rth = (double)sm.rth[vv[r]], dth = th[r] - rth;
+          J += 0.5 * (q0 * dx * dx + q1 * dy * dy + q2 * dth * dth);
+          const double wx = sm.rx[vv[r]] + X0, wy = sm.ry[vv[r]] + Y0;
+          Cr += 0.5 * (q0 * wx * wx + q1 * wy * wy + q2 * rth * rth);
+        }
+      }
+      if (lane == 0) {  // stage 0: x_0 = x0 (fixed by the dynamics rows) against x_ref[0]
+        const double e0 = X0 - (double)x00[0], e1 = Y0 - (double)x00[1], e2 = (double)fTH0 - (double)x00[2];
+        J += 0.5 * (q0 * e0 * e0 + q1 * e1 * e1 + q2 * e2 * e2);
+        const double w0 = x00[0], w1 = x00[1], w2 = x00[2];
+        Cr += 0.5 * (q0 * w0 * w0 + q1 * w1 * w1 + q2 * w2 * w2);
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        J += __shfl_xor(J, o);
+        Cr += __shfl_xor(Cr, o);
+      }
+      const double Cu = 0.5 * (double)N * (P.r[0] * P.udes[0] * P.udes[0] + P.r[1] * P.udes[1] * P.udes[1]);
+      const double dnan = __longlong_as_double(0x7ff8000000000000ll);
+      if (lane == 0 && oo.cost) oo.cost[b] = ok ? J : dnan;
+      if (lane == 0 && oo.obj) oo.obj[b] = ok ? J - Cr - Cu : dnan;
+    }
   }
   if (lane == 0) {
     status_out[b] = status;
@@ -1610,7 +1646,8 @@ __global__ __launch_bounds__(64) F110QP_SOLVE_ATTR void solve_kernel(const KPara
                                                    double* __restrict__ gdbg,
                                                    const WarmState ws,
                                                    const int* __restrict__ list,
-                                                   const int* __restrict__ count) {
+                                                   const int* __restrict__ count,
+                                                   const ObjOut oo) {
   __shared__ Smem<NUM, GAP> sm;
   const int n = list ? __builtin_amdgcn_readfirstlane(*count) : B;
   // XCD-aware order: workgroup i runs on XCD i mod 8, so with one workgroup per QP each XCD
@@ -1623,7 +1660,7 @@ __global__ __launch_bounds__(64) F110QP_SOLVE_ATTR void solve_kernel(const KPara
     const int b = list ? __builtin_amdgcn_readfirstlane(list[item])
                        : (xcd ? xi * per + (xi < rem ? xi : rem) + (item >> 3) : item);
     solve_qp<NUM, GAP>(sm, b, P, x0g, ulg, xrg, hsg, uout, xout, status_out, iters_out, Hdbg,
-                       gdbg, ws);
+                       gdbg, ws, oo);
     wsync();
   }
 }
@@ -1648,7 +1685,7 @@ __global__ __launch_bounds__(64) void group_prep_kernel(const KParams P, const i
     return;
   }
   solve_qp<NUM, GAP>(sm, b, P, x0g, ulg, xrg, hsg, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, ws, g);
+                     nullptr, ws, ObjOut(), g);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1658,9 +1695,9 @@ template <int NUM, bool GAP>
 hipError_t launch_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                     const float* hs, float* uo, float* xo, int* st, int* its, double* Hd,
                     double* gd, const WarmState& ws, const int* list, const int* count, int grid,
-                    hipStream_t s) {
+                    const ObjOut& oo, hipStream_t s) {
   hipLaunchKernelGGL((solve_kernel<NUM, GAP>), dim3(grid), dim3(64), 0, s, P, B, x0, ul, xr, hs,
-                     uo, xo, st, its, Hd, gd, ws, list, count);
+                     uo, xo, st, its, Hd, gd, ws, list, count, oo);
   return hipGetLastError();
 }
 

@@ -65,7 +65,14 @@ EXPORTED = (
     "f110qp_parse_waypoints",
     "f110qp_plan_batch_dev",
     "f110qp_plan_batch",
+    "f110qp_solve_batch_ex",
+    "f110qp_solve_batch_ex_dev",
+    "f110qp_solve_grouped_ex",
+    "f110qp_solve_grouped_ex_dev",
+    "f110qp_select_dev",
+    "f110qp_backend_info",
 )
+SCRATCH_NAMES = {0: "none (wave back end)", 1: "LDS fp64", 2: "LDS fp32", 3: "HBM fp64", 4: "HBM fp32"}
 
 
 class Config(C.Structure):
@@ -125,6 +132,12 @@ def load():
     L.f110qp_solve_batch_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 9
     L.f110qp_solve_grouped.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 4
     L.f110qp_solve_grouped_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 5
+    L.f110qp_solve_batch_ex.argtypes = [C.c_void_p, C.c_int] + [fp] * 10
+    L.f110qp_solve_batch_ex_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 11
+    L.f110qp_solve_grouped_ex.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 6
+    L.f110qp_solve_grouped_ex_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 7
+    L.f110qp_select_dev.argtypes = [C.c_int, fp, C.c_int, fp, fp, fp, fp, fp]
+    L.f110qp_backend_info.argtypes = [C.c_void_p, C.c_int, C.c_int] + [C.POINTER(C.c_int)] * 3
     L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
     L.f110qp_warm_reset.argtypes = [C.c_void_p]
     L.f110qp_qp_dims.argtypes = [C.c_int] + [C.POINTER(C.c_int)] * 4
@@ -206,9 +219,17 @@ class Solver:
         except Exception:
             pass
 
-    def solve(self, x0, u_lin, x_ref, halfspace=None):
+    def backend_info(self, batch: int, grouped: bool = False):
+        """(backend, qps_per_wave, scratch) of a solve call of `batch` QPs (f110qp_backend_info)."""
+        v = [C.c_int() for _ in range(3)]
+        _check(self.lib.f110qp_backend_info(self._h, int(batch), int(grouped), *[C.byref(x) for x in v]),
+               "f110qp_backend_info")
+        return tuple(x.value for x in v)
+
+    def solve(self, x0, u_lin, x_ref, halfspace=None, objective=False):
         """Host arrays in, host arrays out (synchronous). Returns (u[B,N,2], x[B,N+1,3],
-        status[B], iters[B])."""
+        status[B], iters[B]) and, with objective=True, also (obj[B], cost[B]) float64
+        (f110qp_solve_batch_ex)."""
         N = self.horizon
         x0 = np.ascontiguousarray(x0, np.float32).reshape(-1, 3)
         B = x0.shape[0]
@@ -220,18 +241,32 @@ class Solver:
         x = np.empty((B, N + 1, 3), np.float32)
         st = np.empty(B, np.int32)
         it = np.empty(B, np.int32)
+        if objective:
+            ob = np.empty(B, np.float64)
+            co = np.empty(B, np.float64)
+            _check(self.lib.f110qp_solve_batch_ex(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(u), _p(x),
+                                                  _p(st), _p(it), _p(ob), _p(co)), "f110qp_solve_batch_ex")
+            return u, x, st, it, ob, co
         _check(self.lib.f110qp_solve_batch(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(u), _p(x),
                                            _p(st), _p(it)), "f110qp_solve_batch")
         return u, x, st, it
 
-    def solve_dev(self, x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters=None, stream=None):
+    def solve_dev(self, x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters=None, stream=None,
+                  obj=None, cost=None):
         """Device (torch) tensors in/out, enqueued on `stream` (torch.cuda stream or None =
-        current stream). Asynchronous."""
+        current stream). Asynchronous. obj / cost: optional float64 [B] device tensors
+        (f110qp_solve_batch_ex_dev)."""
         import torch
 
         B = x0.shape[0]
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
+        if obj is not None or cost is not None:
+            _check(self.lib.f110qp_solve_batch_ex_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
+                                                      _tp(u_out), _tp(x_out), _tp(status), _tp(iters), _tp(obj),
+                                                      _tp(cost), C.c_void_p(stream.cuda_stream)),
+                   "f110qp_solve_batch_ex_dev")
+            return
         _check(self.lib.f110qp_solve_batch_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
                                                _tp(u_out), _tp(x_out), _tp(status), _tp(iters),
                                                C.c_void_p(stream.cuda_stream)), "f110qp_solve_batch_dev")
@@ -300,8 +335,9 @@ class Solver:
         torch.cuda.synchronize(dev)
         return {k: v.cpu().numpy() for k, v in out.items()}
 
-    def solve_grouped(self, x0, u_lin, x_ref, group, num_groups=None, halfspace=None):
-        """Grouped solve on host arrays (f110qp_solve_grouped): group [B] int scenario ids."""
+    def solve_grouped(self, x0, u_lin, x_ref, group, num_groups=None, halfspace=None, objective=False):
+        """Grouped solve on host arrays (f110qp_solve_grouped): group [B] int scenario ids.
+        objective=True also returns (obj[B], cost[B]) (f110qp_solve_grouped_ex)."""
         N = self.horizon
         x0 = np.ascontiguousarray(x0, np.float32).reshape(-1, 3)
         B = x0.shape[0]
@@ -315,18 +351,31 @@ class Solver:
         x = np.empty((B, N + 1, 3), np.float32)
         st = np.empty(B, np.int32)
         it = np.empty(B, np.int32)
+        if objective:
+            ob = np.empty(B, np.float64)
+            co = np.empty(B, np.float64)
+            _check(self.lib.f110qp_solve_grouped_ex(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(g), G, _p(u),
+                                                    _p(x), _p(st), _p(it), _p(ob), _p(co)), "f110qp_solve_grouped_ex")
+            return u, x, st, it, ob, co
         _check(self.lib.f110qp_solve_grouped(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(g), G, _p(u), _p(x),
                                              _p(st), _p(it)), "f110qp_solve_grouped")
         return u, x, st, it
 
     def solve_grouped_dev(self, x0, u_lin, x_ref, halfspace, group, num_groups, u_out, x_out, status, iters=None,
-                          stream=None):
-        """Grouped solve on device (torch) tensors; group [B] int32 on the device."""
+                          stream=None, obj=None, cost=None):
+        """Grouped solve on device (torch) tensors; group [B] int32 on the device; obj / cost
+        optional float64 [B] (f110qp_solve_grouped_ex_dev)."""
         import torch
 
         B = x0.shape[0]
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
+        if obj is not None or cost is not None:
+            _check(self.lib.f110qp_solve_grouped_ex_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
+                                                        _tp(group), int(num_groups), _tp(u_out), _tp(x_out),
+                                                        _tp(status), _tp(iters), _tp(obj), _tp(cost),
+                                                        C.c_void_p(stream.cuda_stream)), "f110qp_solve_grouped_ex_dev")
+            return
         _check(self.lib.f110qp_solve_grouped_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
                                                  _tp(group), int(num_groups), _tp(u_out), _tp(x_out), _tp(status),
                                                  _tp(iters), C.c_void_p(stream.cuda_stream)),
@@ -344,6 +393,18 @@ class Solver:
         _check(self.lib.f110qp_condense_debug_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(H_out),
                                                   _tp(g_out), C.c_void_p(stream.cuda_stream)),
                "f110qp_condense_debug_dev")
+
+
+def select_dev(group, num_groups, cost, status, winner, best_cost, stream=None):
+    """Per-scenario argmin on the device (f110qp_select_dev): group [B] i32, cost [B] f64,
+    status [B] i32 -> winner [G] i32 (-1: no solved candidate), best_cost [G] f64."""
+    import torch
+
+    if stream is None:
+        stream = torch.cuda.current_stream(cost.device)
+    _check(load().f110qp_select_dev(int(group.shape[0]), _tp(group), int(num_groups), _tp(cost), _tp(status),
+                                    _tp(winner), _tp(best_cost), C.c_void_p(stream.cuda_stream)),
+           "f110qp_select_dev")
 
 
 def find_half_spaces(state, ranges, angle_min, angle_inc, angle_max, thresh=3.0, divider=1.5, buffer=3.0):

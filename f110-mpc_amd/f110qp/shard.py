@@ -3,8 +3,10 @@
 QPs are independent, so a global batch is split into contiguous per-rank ranges with no
 collective on the data path. Ranges are aligned to the candidate-group size (e.g. 120
 candidates of one scenario share x0 and the linearisation point) so that a scenario never
-straddles two GPUs. The only collective is the optional result gather to every rank
-(all_gather over RCCL/xGMI on GPUs, gloo in the CPU tests): a few KB per QP batch.
+straddles two GPUs. The collectives are the optional result gather to every rank (all_gather
+over RCCL/xGMI on GPUs, gloo in the CPU tests: a few KB per QP batch) and the per-scenario
+min-loc of the downstream selection (select_sharded: two all_reduce MIN over [scenarios] words),
+needed when a scenario's candidates straddle ranks (any split not aligned to the scenarios).
 """
 from __future__ import annotations
 
@@ -50,3 +52,31 @@ def solve_sharded(solve_fn: Callable[[Dict], Dict], inputs: Dict, group_align: i
         dist.all_gather(bufs, pad, group=pg)
         res[k] = torch.cat([b[: h - l] for b, (l, h) in zip(bufs, sizes)], 0)
     return res
+
+
+INDEX_NONE = (1 << 62)  # "no solved candidate on this rank" in the index all-reduce
+
+
+def select_sharded(best, winner, pg=None):
+    """Min-loc over the ranks of the per-scenario selection: every rank
+    holds, for ALL scenarios g (global ids), its local best cost best[g] (float64, +inf when it
+    has no solved candidate of g) and the GLOBAL index winner[g] of that candidate (int, -1 none),
+    e.g. from f110qp_select_dev on its shard plus the shard offset. Returns the global (best,
+    winner) on every rank: the minimal cost over all ranks, ties to the smallest global index,
+    i.e. exactly what one process selecting over the whole batch returns. Two all_reduce(MIN)
+    of G words each (RCCL over xGMI with the nccl backend: device tensors; gloo: host tensors)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized() or dist.get_world_size(pg) == 1:
+        return best, winner
+    on_dev = dist.get_backend(pg) == "nccl"
+    dev = best.device if on_dev else torch.device("cpu")
+    b = best.to(dev, torch.float64).clone()
+    w = winner.to(dev, torch.int64)
+    dist.all_reduce(b, op=dist.ReduceOp.MIN, group=pg)
+    mine = (w >= 0) & (best.to(dev, torch.float64) == b)
+    idx = torch.where(mine, w, torch.full_like(w, INDEX_NONE))
+    dist.all_reduce(idx, op=dist.ReduceOp.MIN, group=pg)
+    idx = torch.where(idx == INDEX_NONE, torch.full_like(idx, -1), idx)
+    return b.to(best.device), idx.to(winner.device)

@@ -38,7 +38,16 @@
  *                            the final one that confirms the KKT point (0 would mean none ran);
  *                            QPs the wave back end hands to its Goldfarb-Idnani loop (gap rows,
  *                            or a box PDAS that did not settle) count GI iterations instead
- *    On a non-SOLVED status u_out/x_out hold NaN, as OSQP's solution does on failure.
+ *      obj       [B] double  (the *_ex entry points; may be NULL) OSQP's objective value
+ *                            1/2 z'Pz + q'z of the solved QP (osqp_info::obj_val; P, q of
+ *                            mpc.cpp:208-229), computed in fp64 on the device
+ *      cost      [B] double  (*_ex; may be NULL) the same objective WITH the constant OSQP drops:
+ *                            sum_i 1/2|x_i - x_ref_i|_Q^2 + sum_k 1/2|u_k - u_des|_R^2 >= 0
+ *                            (= obj + 1/2 sum_i x_ref_i'Q x_ref_i + N/2 u_des'R u_des). Candidates
+ *                            with different references are compared on `cost`: obj carries the
+ *                            reference-dependent constant -1/2 sum x_ref'Q x_ref.
+ *    On a non-SOLVED status u_out/x_out hold NaN (obj/cost too), as OSQP's solution does on
+ *    failure.
  */
 #ifndef F110QP_H
 #define F110QP_H
@@ -47,7 +56,7 @@
 extern "C" {
 #endif
 
-#define F110QP_API_VERSION 4
+#define F110QP_API_VERSION 5
 
 /* return codes */
 #define F110QP_OK 0
@@ -153,6 +162,42 @@ int f110qp_solve_grouped_dev(f110qp_ctx* ctx, int batch, const float* x0, const 
                              const float* x_ref, const float* halfspace, const int* group,
                              int num_groups, float* u_out, float* x_out, int* status, int* iters,
                              void* stream);
+
+/* Same as f110qp_solve_batch[_dev] / f110qp_solve_grouped[_dev], plus the per-QP objective
+ * `obj` and `cost` (see Layouts; either may be NULL). The objective is what
+ * OsqpEigen::Solver::solve() leaves in osqp_info::obj_val after src/mpc.cpp:133. */
+int f110qp_solve_batch_ex(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                          const float* x_ref, const float* halfspace, float* u_out, float* x_out,
+                          int* status, int* iters, double* obj, double* cost);
+int f110qp_solve_batch_ex_dev(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                              const float* x_ref, const float* halfspace, float* u_out,
+                              float* x_out, int* status, int* iters, double* obj, double* cost,
+                              void* stream);
+int f110qp_solve_grouped_ex(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                            const float* x_ref, const float* halfspace, const int* group,
+                            int num_groups, float* u_out, float* x_out, int* status, int* iters,
+                            double* obj, double* cost);
+int f110qp_solve_grouped_ex_dev(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                                const float* x_ref, const float* halfspace, const int* group,
+                                int num_groups, float* u_out, float* x_out, int* status,
+                                int* iters, double* obj, double* cost, void* stream);
+
+/* Per-scenario selection on the device: the candidate argmin of
+ * project::OdomCallback (src/project.cpp:125-136), taken over the QP costs of each scenario's
+ * candidates instead of the end-point distance. winner[g] = the smallest b with group[b] == g,
+ * status[b] == F110QP_SOLVED and the minimal cost[b] (exact, deterministic), or -1 when the
+ * scenario has no solved candidate; best_cost[g] = that cost (+inf if none). group/cost/status
+ * [batch], winner/best_cost [num_groups], device pointers, async on stream. Across GPUs, the
+ * per-rank (best_cost, winner) pairs reduce with a min-loc all-reduce (f110qp/shard.py). */
+int f110qp_select_dev(int batch, const int* group, int num_groups, const double* cost,
+                      const int* status, int* winner, double* best_cost, void* stream);
+
+/* The launch a solve call of `batch` QPs on this context makes (grouped != 0: the grouped entry
+ * points): backend = F110QP_BACKEND_WAVE or _LANE (what AUTO resolves to), qps_per_wave (lane:
+ * QPs per 64-lane wavefront; wave: 1) and scratch (lane: 1 LDS fp64, 2 LDS fp32, 3 HBM fp64,
+ * 4 HBM fp32 Riccati gain scratch; wave: 0). Any pointer may be NULL. */
+int f110qp_backend_info(f110qp_ctx* ctx, int batch, int grouped, int* backend, int* qps_per_wave,
+                        int* scratch);
 
 /* Forget the warm-start state of every slot (the next call solves cold). */
 int f110qp_warm_reset(f110qp_ctx* ctx);

@@ -593,6 +593,14 @@ void f110o_kkt_residuals(const f110o_params* prm, const double x0[3], const doub
 int f110o_solve_batch(const f110o_params* prm, int batch, const float* x0, const float* ulin,
                       const float* x_ref, const float* hs, int gap_active, double* u_out,
                       double* x_out, int* status, int num_threads) {
+  return f110o_solve_batch_obj(prm, batch, x0, ulin, x_ref, hs, gap_active, u_out, x_out, status,
+                               NULL, num_threads);
+}
+
+/* the same with OSQP's objective 0.5 z'Pz + q'z per QP (obj_out may be NULL) */
+int f110o_solve_batch_obj(const f110o_params* prm, int batch, const float* x0, const float* ulin,
+                          const float* x_ref, const float* hs, int gap_active, double* u_out,
+                          double* x_out, int* status, double* obj_out, int num_threads) {
   const int N = prm->horizon;
   int nsolved = 0;
 #ifdef _OPENMP
@@ -608,7 +616,8 @@ int f110o_solve_batch(const f110o_params* prm, int batch, const float* x0, const
     if (hs) for (int k = 0; k < 6; k++) hh[k] = hs[6 * b + k];
     int st = f110o_solve(prm, xx, uu, xr, hs ? hh : NULL, gap_active,
                          u_out ? u_out + (size_t)b * 2 * N : NULL,
-                         x_out ? x_out + (size_t)b * 3 * (N + 1) : NULL, NULL, NULL, NULL, NULL);
+                         x_out ? x_out + (size_t)b * 3 * (N + 1) : NULL, NULL, NULL,
+                         obj_out ? obj_out + b : NULL, NULL);
     if (status) status[b] = st;
     nsolved += (st == F110O_SOLVED);
     free(xr);

@@ -100,6 +100,9 @@ void f110o_kkt_residuals(const f110o_params* prm, const double x0[3], const doub
 int f110o_solve_batch(const f110o_params* prm, int batch, const float* x0, const float* u_lin,
                       const float* x_ref, const float* hs, int gap_active, double* u_out,
                       double* x_out, int* status, int num_threads);
+int f110o_solve_batch_obj(const f110o_params* prm, int batch, const float* x0, const float* u_lin,
+                          const float* x_ref, const float* hs, int gap_active, double* u_out,
+                          double* x_out, int* status, double* obj_out, int num_threads);
 
 /* OSQP-0.6-default-settings ADMM on the sparse formulation (CPU baseline; see osqp_admm.c). */
 typedef struct {

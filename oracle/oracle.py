@@ -102,6 +102,8 @@ def lib():
         L.f110o_kkt_residuals.argtypes = [C.POINTER(Params), dp, dp, dp, dp, C.c_int, dp, dp, dp]
         L.f110o_solve_batch.argtypes = [C.POINTER(Params), C.c_int, fp, fp, fp, fp, C.c_int, dp,
                                         dp, ip, C.c_int]
+        L.f110o_solve_batch_obj.argtypes = [C.POINTER(Params), C.c_int, fp, fp, fp, fp, C.c_int, dp,
+                                            dp, ip, dp, C.c_int]
         if hasattr(L, "f110o_admm_solve_batch"):
             L.f110o_admm_default_settings.argtypes = [C.POINTER(AdmmSettings)]
             L.f110o_admm_solve.argtypes = [C.POINTER(Params), C.POINTER(AdmmSettings), dp, dp, dp,
@@ -230,8 +232,9 @@ def kkt_residuals(prm: Params, x0, u_lin, x_ref, z, y, hs=None, gap_active=False
     return res
 
 
-def solve_batch(prm: Params, x0, u_lin, x_ref, hs=None, gap_active=False, num_threads=0):
-    """Exact batched solve on float32 ABI-layout inputs. Returns (u[B,N,2], x[B,N+1,3], status[B])."""
+def solve_batch(prm: Params, x0, u_lin, x_ref, hs=None, gap_active=False, num_threads=0, objective=False):
+    """Exact batched solve on float32 ABI-layout inputs. Returns (u[B,N,2], x[B,N+1,3], status[B])
+    and, with objective=True, also obj[B] = OSQP's 1/2 z'Pz + q'z at the exact optimum."""
     N = prm.horizon
     x0 = np.ascontiguousarray(x0, np.float32)
     B = x0.shape[0]
@@ -243,9 +246,52 @@ def solve_batch(prm: Params, x0, u_lin, x_ref, hs=None, gap_active=False, num_th
     x = np.zeros((B, N + 1, 3))
     st = np.zeros(B, np.int32)
     fp = C.c_float
-    lib().f110o_solve_batch(C.byref(prm), B, _ptr(x0, fp), _ptr(ul, fp), _ptr(xr, fp), _ptr(h, fp),
-                            int(gap_active), _ptr(u), _ptr(x), _ptr(st, C.c_int), int(num_threads))
+    ob = np.zeros(B) if objective else None
+    lib().f110o_solve_batch_obj(C.byref(prm), B, _ptr(x0, fp), _ptr(ul, fp), _ptr(xr, fp), _ptr(h, fp),
+                                int(gap_active), _ptr(u), _ptr(x), _ptr(st, C.c_int), _ptr(ob), int(num_threads))
+    if objective:
+        return u, x, st, ob
     return u, x, st
+
+
+def tracking_cost(prm: Params, u, x, x_ref):
+    """sum_{i=0..N} 1/2|x_i - r_i|_Q^2 + sum_k 1/2|u_k - u_des|_R^2 of solutions u [B,N,2], x [B,N+1,3]
+    (r_N = x_ref[N-1], mpc.cpp:228), float64: the `cost` output of f110qp_solve_*_ex, evaluated
+    directly (no cancellation against OSQP's constant-free objective)."""
+    N = prm.horizon
+    xr = np.asarray(x_ref, np.float64)[:, :N]
+    r_ext = np.concatenate([xr, xr[:, N - 1:N]], 1)
+    q = np.array(prm.q[:])
+    r = np.array(prm.r[:])
+    ud = np.array(prm.u_des[:])
+    return 0.5 * (((np.asarray(x, np.float64) - r_ext) ** 2) * q).sum(axis=(1, 2)) + \
+        0.5 * (((np.asarray(u, np.float64) - ud) ** 2) * r).sum(axis=(1, 2))
+
+
+def select(group, num_groups, cost, status):
+    """Per-scenario argmin (the checker of f110qp_select_dev): smallest index among the solved
+    members with the minimal cost; -1 / +inf for a scenario without a solved member."""
+    winner = np.full(num_groups, -1, np.int64)
+    best = np.full(num_groups, np.inf)
+    for b in range(len(group)):
+        g = int(group[b])
+        if 0 <= g < num_groups and status[b] == SOLVED and cost[b] < best[g]:
+            best[g] = cost[b]
+            winner[g] = b
+    return winner, best
+
+
+def cost_from_obj(prm: Params, obj, x_ref):
+    """OSQP's objective plus the constant it drops: obj + 1/2 sum_{i=0..N} r_i'Q r_i + N/2 u_des'R u_des
+    (r_i = x_ref[i], r_N = x_ref[N-1], mpc.cpp:221-229) = the tracking cost sum 1/2|x-r|_Q^2 +
+    1/2|u-u_des|_R^2 of the solution (the `cost` output of f110qp_solve_*_ex)."""
+    N = prm.horizon
+    xr = np.asarray(x_ref, np.float64)[:, :N]
+    q = np.array(prm.q[:])
+    r = np.array(prm.r[:])
+    ud = np.array(prm.u_des[:])
+    c = 0.5 * (xr ** 2 * q).sum(axis=(1, 2)) + 0.5 * (xr[:, N - 1] ** 2 * q).sum(axis=1)
+    return obj + c + 0.5 * N * float((r * ud * ud).sum())
 
 
 def admm_settings(**over) -> AdmmSettings:

@@ -30,7 +30,7 @@ def test_library_is_gfx950_code_object(capi):
 
 def test_version_and_defaults(capi):
     L = capi.load()
-    assert L.f110qp_version() == 4
+    assert L.f110qp_version() == 5
     c = capi.default_config(20)
     # params.yaml:1-13,42-47 and constraints.cpp:19,21
     assert c.horizon == 20 and c.dt == np.float32(0.01)
@@ -135,3 +135,23 @@ def test_qp_dims_match_reference_sizes(capi, oracle):
     nonzeros of P and A, equal to the oracle's assembly for every horizon."""
     for N in (1, 20, 30, 40, 48):
         assert capi.qp_dims(N) == oracle.dims(N)
+
+
+def test_backend_info_resolves_auto_and_scratch(capi):
+    """f110qp_backend_info (host only, no device needed): AUTO resolves to the lane back end at
+    the measured thresholds (F110QP_LANE_MIN_BATCH[_WIDE]), gap rows always to the wave back end;
+    the lane QPs-per-wave fill <= 256 waves; the scratch sits in LDS (fp64 when it fits) while the
+    grid's waves are resident with it and in HBM (fp32) at the C4 size."""
+    s20 = capi.Solver(capi.default_config(20))
+    assert s20.backend_info(1024) == (capi.BACKEND_WAVE, 1, 0)
+    assert s20.backend_info(capi.LANE_MIN_BATCH)[0] == capi.BACKEND_LANE
+    assert s20.backend_info(4096) == (capi.BACKEND_LANE, 16, 1)
+    assert s20.backend_info(65536) == (capi.BACKEND_LANE, 64, 4)
+    s40 = capi.Solver(capi.default_config(40))
+    assert s40.backend_info(capi.LANE_MIN_BATCH_WIDE - 1)[0] == capi.BACKEND_WAVE
+    assert s40.backend_info(8192, grouped=True) == (capi.BACKEND_LANE, 32, 1)
+    assert s40.backend_info(65536, grouped=True) == (capi.BACKEND_LANE, 64, 4)
+    sg = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE))
+    assert sg.backend_info(65536)[0] == capi.BACKEND_WAVE
+    for s in (s20, s40, sg):
+        s.close()

@@ -37,7 +37,8 @@ def check(oracle, capi, N, w, hs=None, gap=False, tol=TOL, **cfg):
     s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, **cfg))
     u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
     s.close()
-    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=gap)
+    over = {k: v for k, v in cfg.items() if k in ("q", "r", "u_des", "u_min", "u_max")}
+    ur, xr, sr = oracle.solve_batch(oracle.params(N, **over), w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=gap)
     np.testing.assert_array_equal(st, sr)
     ok = sr == oracle.SOLVED
     if ok.any():
@@ -288,6 +289,40 @@ def test_half_space_kernel_adversarial(oracle, capi, cuda, nr, seed):
         same += int((hs[b] == ref).all())
         total += 1
     assert total == 0 or same / total >= 0.95, (same, total)
+
+
+def test_half_space_kernel_long_run_and_empty_window(oracle, capi, cuda):
+    """Edge cases of the wave-per-scan gap search: a run of open beams longer than 32,767 (the
+    run key (length << 16 | 65535 - end) must not overflow) and an empty field-of-view window
+    (angle_max < angle_min: no block is loaded, (lo, hi) = (0, 0) and ranges[0] is read, as the
+    reference does). Indices and half-spaces as the reference state machine."""
+    import torch
+
+    nr = 40000
+    amin = np.float32(-1.0)
+    ainc = np.float32(2.0 / (nr - 1))
+    amax = np.float32(amin + ainc * np.float32(nr - 1))
+    r = np.full((3, nr), 5.0, np.float32)
+    r[0, 100] = 1.0          # runs of 99 and 39,899 beams
+    r[1, 36000] = 1.0        # the longest run (35,999 beams) first
+    r[2, :] = 1.0
+    r[2, 5:38000] = 6.0      # one run of 37,995 beams
+    st = np.float32([[1.0, -2.0, 0.3], [0.0, 0.0, 0.0], [-5.0, 4.0, -1.2]])
+    for amax_use in (amax, np.float32(amin - 5 * ainc)):
+        hs = torch.empty((3, 2, 3), dtype=torch.float32, device=cuda)
+        lo = torch.empty(3, dtype=torch.int32, device=cuda)
+        hi = torch.empty(3, dtype=torch.int32, device=cuda)
+        capi.find_half_spaces_dev(torch.from_numpy(st).to(cuda), torch.from_numpy(r).to(cuda), amin, ainc,
+                                  amax_use, hs, lo, hi)
+        torch.cuda.synchronize()
+        hs, lo, hi = hs.cpu().numpy(), lo.cpu().numpy(), hi.cpu().numpy()
+        for b in range(3):
+            rc, l1, l2, rlo, rhi = oracle.find_half_spaces(st[b].astype(np.float64), r[b], amin, ainc, amax_use)
+            assert (lo[b], hi[b]) == (rlo, rhi), (b, lo[b], hi[b], rlo, rhi)
+            if amax_use == amax:
+                assert hi[b] - lo[b] > 32767 - 6, (b, lo[b], hi[b])
+            ref = np.float32([l1, l2])
+            np.testing.assert_allclose(hs[b], ref, rtol=2e-6, atol=2e-6 * np.abs(ref).max())
 
 
 def test_half_space_kernel(oracle, capi, cuda):
@@ -580,6 +615,29 @@ def test_lane_backend_scratch_modes(oracle, capi, monkeypatch, mode):
 
 
 
+@pytest.mark.parametrize("be,mode,kmax", [("wave", "0", "16"), ("lane", "1", "16"), ("lane", "4", "16"),
+                                           ("lane", "1", "0"), ("lane", "4", "0")])
+def test_degenerate_bound_zero_multiplier(oracle, capi, monkeypatch, be, mode, kmax):
+    """u_des = (4.5, 0) with des_vel = umax (params.yaml:42,46): with Q = 0 the optimum is
+    u = u_des at every stage, so the speed sits exactly on its upper bound with a ZERO multiplier
+    (a degenerate complementarity pair), and with a tiny Q it is within rounding of that. The
+    PDAS flip tests carry a tolerance, so rounding noise cannot flip such an input free -> bound
+    -> free until the pass cap (MAX_ITER): every QP must come back SOLVED at the exact optimum,
+    with the multi-flip passes and with single flips from the first pass, fp64 and fp32 gains."""
+    monkeypatch.setenv("F110QP_LANE_MODE", mode)
+    monkeypatch.setenv("F110QP_LANE_KMAX", kmax)
+    N = 20
+    for q in ([0.0, 0.0, 0.0], [1e-9, 1e-9, 0.0], [1e-3, 1e-3, 0.0]):
+        w = workload.make_batch(700, N, seed=4500, heading="true", lateral=0.0, steer_range=0.0)
+        # fp32 gain scratch (mode 4): a degenerate QP settles in the single-flip passes with the
+        # looser fp32 flip tolerance (lane_kernel.h): exact to ~1e-6, inside the 1e-4 bound
+        u, x, st, it = check(oracle, capi, N, w, backend=_be(capi, be), tol=2e-6 if mode != "4" else 1e-5, q=q)
+        assert (st == capi.SOLVED).all(), (q, np.unique(st, return_counts=True))
+        if q[0] == 0.0:
+            np.testing.assert_allclose(u[..., 0], 4.5, atol=1e-5)
+            np.testing.assert_allclose(u[..., 1], 0.0, atol=1e-5)
+
+
 @pytest.mark.parametrize("be", ["wave", "lane"])
 def test_non_finite_inputs_are_numerical(oracle, capi, be):
     """NaN / inf in x0, u_lin or x_ref (the planning stage emits a NaN x_ref when no candidate is
@@ -681,3 +739,85 @@ def test_assembly_hook_matches_reference_layout(oracle, capi, N, gap):
             np.testing.assert_allclose(got[k], ref[k], rtol=1e-15, atol=1e-18, err_msg=k)
         assert (got["A_val"] == 0).sum() == (ref["A_val"] == 0).sum()  # explicit zeros kept
     s.close()
+
+
+@pytest.mark.parametrize("be,gap,N", [("wave", False, 20), ("lane", False, 20), ("lane", False, 40),
+                                      ("wave", True, 20), ("wave", False, 40)])
+def test_objective_matches_oracle(oracle, capi, be, gap, N):
+    """f110qp_solve_batch_ex: obj = OSQP's 1/2 z'Pz + q'z (what osqp_info::obj_val holds after
+    mpc.cpp:133) and cost = the tracking cost (obj plus the constant OSQP drops), both fp64 from
+    the device, against the exact optimum's objective (oracle, f110_oracle.c:544-554) and the
+    tracking cost of the oracle's solution: rel 1e-6 on obj (about |obj| ~ 1e5 in world
+    coordinates) and 1e-6 * max(1, cost) on cost. Non-solved QPs give NaN."""
+    B = 1500
+    w = workload.make_batch(B, N, seed=6060 + N, heading="true", lateral=1.0, steer_range=0.6)
+    hs = None
+    if gap:
+        ranges, amin, ainc, amax = workload.make_scans(B, seed=6061)
+        hs = halfspaces_oracle(oracle, w["x0"], ranges, (amin, ainc, amax))
+    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE,
+                                        backend=_be(capi, be)))
+    u, x, st, it, ob, co = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs, objective=True)
+    s.close()
+    prm = oracle.params(N)
+    ur, xr, sr, obr = oracle.solve_batch(prm, w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=gap, objective=True)
+    np.testing.assert_array_equal(st, sr)
+    ok = sr == oracle.SOLVED
+    assert ok.mean() > 0.9
+    np.testing.assert_allclose(ob[ok], obr[ok], rtol=1e-6, atol=1e-6)
+    cr = oracle.tracking_cost(prm, ur, xr, w["x_ref"])
+    assert (np.abs(co[ok] - cr[ok]) <= 1e-6 * np.maximum(1.0, cr[ok])).all(), np.abs(co[ok] - cr[ok]).max()
+    assert (co[ok] >= 0).all()
+    assert np.isnan(ob[~ok]).all() and np.isnan(co[~ok]).all()
+
+
+@pytest.mark.parametrize("be", ["wave", "lane"])
+def test_select_per_scenario(oracle, capi, cuda, be):
+    """C4 candidate sets (6 lanes x 20 steers per scenario, N = 40) solved grouped with the cost
+    output, then f110qp_select_dev: the winner of every scenario is the argmin of the costs
+    (smallest index on ties: two identical candidates are planted), equal to the argmin of the
+    exact optimum's costs wherever the best two candidates differ by more than the tolerance; a
+    scenario whose candidates are all non-finite gets winner -1 / +inf."""
+    import torch
+
+    N, S = 40, 12
+    g = workload.make_grouped_batch(S, N, seed=7070)
+    G = g["group_size"]
+    w = {k: np.ascontiguousarray(g[k]) for k in ("x0", "u_lin", "x_ref")}
+    B = S * G
+    for k in w:
+        w[k][5 * G + 7] = w[k][5 * G + 3]     # a tie inside scenario 5
+    w["x_ref"][11 * G:12 * G] = np.nan        # scenario 11: no solvable candidate
+    gid_np = (np.arange(B) // G).astype(np.int32)
+    dev = cuda
+    t = {k: torch.from_numpy(v).to(dev) for k, v in w.items()}
+    gid = torch.from_numpy(gid_np).to(dev)
+    uo = torch.empty((B, N, 2), dtype=torch.float32, device=dev)
+    xo = torch.empty((B, N + 1, 3), dtype=torch.float32, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    co = torch.empty(B, dtype=torch.float64, device=dev)
+    s = capi.Solver(capi.default_config(N, backend=_be(capi, be)))
+    s.solve_grouped_dev(t["x0"], t["u_lin"], t["x_ref"], None, gid, S, uo, xo, st, None, cost=co)
+    win = torch.empty(S, dtype=torch.int32, device=dev)
+    best = torch.empty(S, dtype=torch.float64, device=dev)
+    capi.select_dev(gid, S, co, st, win, best)
+    torch.cuda.synchronize()
+    s.close()
+    stn, con, winn, bestn = st.cpu().numpy(), co.cpu().numpy(), win.cpu().numpy(), best.cpu().numpy()
+    w_chk, b_chk = oracle.select(gid_np, S, con, stn)     # the argmin of the device's own costs
+    np.testing.assert_array_equal(winn, w_chk)
+    np.testing.assert_array_equal(bestn, b_chk)
+    assert winn[11] == -1 and np.isinf(bestn[11])
+    assert winn[5] != 5 * G + 7 or con[5 * G + 3] > con[5 * G + 7]
+    prm = oracle.params(N)
+    ur, xr, sr = oracle.solve_batch(prm, w["x0"], w["u_lin"], w["x_ref"])
+    cr = oracle.tracking_cost(prm, ur, xr, w["x_ref"])
+    w_ref, b_ref = oracle.select(gid_np, S, cr, sr)
+    for sc in range(S):
+        if w_ref[sc] < 0:
+            assert winn[sc] == -1
+            continue
+        c = np.sort(cr[sc * G:(sc + 1) * G][sr[sc * G:(sc + 1) * G] == oracle.SOLVED])
+        if len(c) > 1 and c[1] - c[0] > 1e-6 * max(1.0, c[0]):
+            assert winn[sc] == w_ref[sc], (sc, winn[sc], w_ref[sc])
+        assert abs(bestn[sc] - b_ref[sc]) <= 1e-6 * max(1.0, b_ref[sc])

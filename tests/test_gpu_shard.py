@@ -53,3 +53,43 @@ def test_two_rank_hip_shards_bit_equal(capi, cuda, tmp_path, N, scen, be):
     np.testing.assert_array_equal(d["status"], st.cpu().numpy())
     np.testing.assert_array_equal(d["u"], uo.cpu().numpy())
     np.testing.assert_array_equal(d["x"], xo.cpu().numpy())
+
+
+@pytest.mark.parametrize("be", ["lane", "wave"])
+def test_two_rank_select_straddling_scenarios(capi, cuda, tmp_path, be):
+    """The per-scenario selection across ranks when a scenario straddles
+    two GPUs: each rank solves its half (split at a non-multiple of 120) with the cost output and
+    selects per global scenario id on the device, the min-loc all-reduce combines the ranks; the
+    result equals one process selecting over the whole batch, bit for bit."""
+    import torch
+
+    from f110qp import workload
+
+    N, scen = 40, 5
+    backend = {"lane": capi.BACKEND_LANE, "wave": capi.BACKEND_WAVE}[be]
+    out = tmp_path / "select.npz"
+    env = {**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                    os.path.join(ROOT, "tests", "shard_gpu_worker.py"), str(out), str(N), str(scen), str(backend),
+                    "select"], check=True, timeout=180, env=env, cwd=ROOT)
+    d = np.load(out)
+    assert int(d["world"]) == 2 and int(d["lo1"]) % 120 != 0  # scenario 2 straddles the ranks
+    g = workload.make_grouped_batch(scen, N, seed=4242)
+    B = g["x0"].shape[0]
+    dev = torch.device("cuda", 0)
+    x0, ul, xr = (torch.from_numpy(np.ascontiguousarray(g[k])).to(dev) for k in ("x0", "u_lin", "x_ref"))
+    gid = (torch.arange(B, dtype=torch.int32) // g["group_size"]).to(dev)
+    uo = torch.empty((B, N, 2), dtype=torch.float32, device=dev)
+    xo = torch.empty((B, N + 1, 3), dtype=torch.float32, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    co = torch.empty(B, dtype=torch.float64, device=dev)
+    s = capi.Solver(capi.default_config(N, device=0, backend=backend))
+    s.solve_dev(x0, ul, xr, None, uo, xo, st, None, cost=co)
+    win = torch.empty(scen, dtype=torch.int32, device=dev)
+    best = torch.empty(scen, dtype=torch.float64, device=dev)
+    capi.select_dev(gid, scen, co, st, win, best)
+    torch.cuda.synchronize()
+    s.close()
+    np.testing.assert_array_equal(d["winner"], win.cpu().numpy().astype(np.int64))
+    np.testing.assert_array_equal(d["best"], best.cpu().numpy())
