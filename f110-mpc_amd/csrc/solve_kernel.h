@@ -970,6 +970,59 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 
   STAMP_SET(t_inv);
   inputs_and_gradient();
+  // GAP: steepest-edge ranking of the gap rows in GI's step 1. A gap row of stage k+1
+  // (mpc.cpp:249,271) is n_j'u >= beta_j with n_j = Gamma_{k+1}'(a, b, 0), which by A = I + E
+  // (model.cpp:42-51) is n_j = alpha u + beta (k p - r) on the inputs of stages <= k, with
+  // u = [speed input], p = (b20 | b21) by input, r = stage * p. Its W-norm n_j'W n_j then follows
+  // from six block moments M_xy(k) = sum_{w,v of stages <= k} x_w W_wv y_v (x, y in {u, p, r}),
+  // which one pass over each lane's row of W and six wave prefix scans give for every k. Ranking
+  // the violated gap rows by slack / sqrt(n_j'W n_j) instead of slack / |(a, b)| cut the GI
+  // iterations of the bench's C3 batch from max 58 / p99 21 to 34 / 17 (numpy model of this
+  // loop, box rows kept at slack / (1 + |bound|)): C3's time is its slowest QP's GI chain.
+  float gsc[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) gsc[r] = 0.f;
+  if constexpr (GAP) {
+    const Lin M = sm.M;
+    double T[6][R];  // per variable w: its part of the moments uu, up, ur, pp, pr, rr
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int kw = kk[r];
+      const double pw = valid[r] ? (a ? M.b21 : M.b20) : 0.0, uw = (valid[r] && a == 0) ? 1.0 : 0.0;
+      const double rw = kw * pw;
+      float RPu = 0.f, RPp = 0.f, RPr = 0.f, SSu = 0.f, SSp = 0.f, SSr = 0.f;
+      const float fb20 = (float)M.b20, fb21 = (float)M.b21;
+      for (int x = 0; x < NUM; x++) {  // W[w][x] = sm.W[x][w]: consecutive lanes, conflict free
+        const float wx = (x <= 2 * kw + 1) ? sm.W[x][cl[r]] : 0.f;
+        const int kx = x >> 1;
+        const float px = (x & 1) ? fb21 : fb20, ux = (x & 1) ? 0.f : 1.f, rx = (float)kx * px;
+        RPu = fmaf(wx, ux, RPu); RPp = fmaf(wx, px, RPp); RPr = fmaf(wx, rx, RPr);
+        const float ws = (kx == kw) ? wx : 0.f;
+        SSu = fmaf(ws, ux, SSu); SSp = fmaf(ws, px, SSp); SSr = fmaf(ws, rx, SSr);
+      }
+      // pairs (w, x) with stage(x) <= stage(w) from row w, pairs with stage(w) < stage(x) from row x
+      const double Su = RPu - SSu, Sp = RPp - SSp, Sr = RPr - SSr;
+      T[0][r] = uw * RPu + uw * Su;
+      T[1][r] = uw * RPp + pw * Su;
+      T[2][r] = uw * RPr + rw * Su;
+      T[3][r] = pw * RPp + pw * Sp;
+      T[4][r] = pw * RPr + rw * Sp;
+      T[5][r] = rw * RPr + rw * Sr;
+    }
+#pragma unroll
+    for (int m = 0; m < 6; m++) scan_incl_R<R>(T[m]);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      double Mm[6];
+#pragma unroll
+      for (int m = 0; m < 6; m++) Mm[m] = odd_lane(T[m][r]);  // stage k's moments sit in lane 2k+1
+      const double ah = a ? ga1 : ga0, bh = a ? gb1 : gb0;
+      const double al = ah * M.b00 + bh * M.b10, be = ah * M.a02 + bh * M.a12, k = (double)kk[r];
+      const double c = al * al * Mm[0] + 2.0 * al * be * (k * Mm[1] - Mm[2]) +
+                       be * be * (k * k * Mm[3] - 2.0 * k * Mm[4] + Mm[5]);
+      gsc[r] = (valid[r] && c > 0.0) ? (float)(1.0 / sqrt(c)) : 1.f / gnorm;
+    }
+  }
   STAMP(t_grad);
   // ---- 4. active set -----------------------------------------------------------------------
   float xv[R];           // GI iterate (fp32)
@@ -1208,8 +1261,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         if (!(actf[r] & 2) && v1 < -1e-6f && v1 < best) { best = v1; bid = 3 * v + 1; sraw = s1; }
         if (GAP) {
           const float s2 = (a ? ga1 : ga0) * X[r] + (a ? gb1 : gb0) * Y[r] + cgap[r];
-          const float v2 = s2 / gnorm;
-          if (!(actf[r] & 4) && v2 < -1e-6f && v2 < best) { best = v2; bid = 3 * v + 2; sraw = s2; }
+          const float v2 = s2 * gsc[r];  // ranked by the W-norm (steepest edge), thresholded as before
+          if (!(actf[r] & 4) && s2 < -1e-6f * gnorm && v2 < best) { best = v2; bid = 3 * v + 2; sraw = s2; }
         }
       }
       int bid_w = bid;
