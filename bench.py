@@ -159,10 +159,21 @@ def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int, c
     # per-GPU share (OMP_NUM_THREADS on the GPU box) is smaller than that
     full = None
     if full_threads > threads:
-        nf, elf, _, _ = _admm_rate(oracle, prm, st, w, hs, gap, full_threads, max(3.0, seconds / 3), B)
-        full = {"value": nf / elf, "unit": "QP solves/s", "cores": full_threads,
-                "sample": f"{nf} QPs ({nf // B} x {B} {config} ticks) in {elf:.1f} s, same solver, "
-                          f"OpenMP over {full_threads} threads (every CPU in this process's affinity mask)"}
+        # a bigger batch per call (OpenMP team start-up amortised over more QPs) and a sweep of
+        # thread counts up to every CPU of the affinity mask: the box is shared with other GPUs'
+        # jobs, so the best count is reported with the whole sweep
+        Bf = 16384
+        wf = workload.make_batch(Bf, N, seed=12346)
+        hsf = _halfspaces_host(wf, Bf) if gap else None
+        sweep = {}
+        for t in sorted({min(full_threads, k) for k in (64, 128, full_threads)}):
+            nf, elf, _, _ = _admm_rate(oracle, prm, st, wf, hsf, gap, t, 2.0, Bf)
+            sweep[t] = nf / elf
+        tb = max(sweep, key=sweep.get)
+        full = {"value": sweep[tb], "unit": "QP solves/s", "cores": tb,
+                "threads_sweep": {str(k): v for k, v in sweep.items()}, "affinity_cpus": full_threads,
+                "sample": f"batches of {Bf} {config} ticks (horizon {N}), >= 2 s per thread count, same solver, "
+                          f"OpenMP; best of the sweep reported (the GPU box's CPUs are shared with other jobs)"}
     # the exact solver (the parity oracle) on the same sample, for reference
     n2 = 0
     t1 = time.perf_counter()
@@ -198,7 +209,7 @@ def cpu_baseline(config: str, N: int, gap: bool, seconds: float, threads: int, c
     if full is not None:
         out["full_host"] = full
         out["note"] = (f"value/cores = the per-GPU CPU share ({threads} threads = OMP_NUM_THREADS on the GPU box); "
-                       f"full_host = all {full_threads} CPUs of the affinity mask")
+                       f"full_host = the best of a thread sweep up to all {full_threads} CPUs of the affinity mask")
     return out
 
 
