@@ -27,6 +27,6 @@ for c in c2 c3 c4 c5 c2_big; do bash tools/profile_round.sh $c || exit 6; done
 PROF_NAME=c4_8192 bash tools/profile_round.sh c4 --batch 8192 || exit 7
 for c in c2 c4; do
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29517 \
-    bench.py --gpus 2 --config $c --dist-backend gloo --no-cpu --no-latency --steps 20 > $out/bench_2rank_gloo_$c.json 2> $out/bench_2rank_$c.err || exit 8
+    bench.py --gpus 2 --config $c --dist-backend gloo --no-cpu --no-latency --steps 20 2> $out/bench_2rank_$c.err | grep "^{\"metric\"" > $out/bench_2rank_gloo_$c.json || exit 8
 done
 echo evidence done
