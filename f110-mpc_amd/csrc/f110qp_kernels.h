@@ -7,6 +7,7 @@ namespace f110qp {
 
 // per-QP status ids (== F110QP_* in include/f110qp.h)
 constexpr int F110QP_SOLVED_ID = 1;
+constexpr int F110QP_SOLVED_INACCURATE_ID = 2;
 constexpr int F110QP_MAX_ITER_ID = -2;
 constexpr int F110QP_PRIMAL_INFEASIBLE_ID = -3;
 constexpr int F110QP_NUMERICAL_ID = -10;

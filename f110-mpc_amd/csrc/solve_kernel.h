@@ -321,8 +321,6 @@ struct Smem {
                                    // of two floats is not always a float)
   float rth[VN];
   float cmult[3 * VN];             // multiplier per constraint id
-  int ids[VN];                     // PDAS: constraint id of each active slot
-  float pmu[VN];                   // PDAS: multiplier of each variable's active bound
   alignas(16) float prow[NUM];     // box PDAS: pivot row of T broadcast (pivot_T)
   alignas(16) float yb[NUM];       // box PDAS: right-hand side broadcast (matvec_T)
   double d64[VN];
@@ -397,51 +395,6 @@ __device__ __forceinline__ void tri_backward(Smem<NUM, GAP>& sm, int lane, int q
     const float rj = readlane_f(t, jj);
     out[0] = (lane == jj) ? t : out[0];
     acc[0] = fmaf(-sm.L[jj][col[0]], rj, acc[0]);
-  }
-}
-
-// S_A[i][c] for box slot row i (constraint id sid_i) and uniform slot c: signed entries of W
-template <int NUM, bool GAP>
-__device__ __forceinline__ float s_entry(Smem<NUM, GAP>& sm, int row, int sid_i, int sid_c, int c) {
-  const int vi = sid_i / 3, vc = sid_c / 3;
-  return box_sign(sid_i) * box_sign(sid_c) * sm.W[vi][vc];
-}
-
-// L = chol(S_A) of the q active box slots (left-looking, one lane per slot row, L in LDS): the
-// box PDAS hand-over. Sets this lane's 1/L[j][j] for its slots j < q (other entries keep their
-// value). GI itself only appends a row (step 2) or deletes one (chol_delete).
-template <int NUM, bool GAP, int R>
-__device__ __forceinline__ void chol_slots(Smem<NUM, GAP>& sm, int lane, int q,
-                                           const int (&slot_id)[R], float (&rd)[R]) {
-  static_assert(!GAP, "gap-row slots are factored incrementally");
-  for (int c = 0; c < q; c++) {
-    const int sid_c = GAP ? 0 : rl_i<R>(slot_id, c);
-    float s[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      s[r] = 0.f;
-      const int row = 64 * r + lane;
-      if (row < q && row >= c) {
-        float s0 = s_entry<NUM, GAP>(sm, row, slot_id[r], sid_c, c), s1 = 0.f, s2 = 0.f, s3 = 0.f;
-        int i2 = 0;
-        for (; i2 + 4 <= c; i2 += 4) {  // four independent chains: the LDS reads pipeline
-          s0 = fmaf(-sm.L[row][i2 + 0], sm.L[c][i2 + 0], s0);
-          s1 = fmaf(-sm.L[row][i2 + 1], sm.L[c][i2 + 1], s1);
-          s2 = fmaf(-sm.L[row][i2 + 2], sm.L[c][i2 + 2], s2);
-          s3 = fmaf(-sm.L[row][i2 + 3], sm.L[c][i2 + 3], s3);
-        }
-        for (; i2 < c; i2++) s0 = fmaf(-sm.L[row][i2], sm.L[c][i2], s0);
-        s[r] = (s0 + s1) + (s2 + s3);
-      }
-    }
-    const float dcc = sqrtf(rl_f<R>(s, c));
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const int row = 64 * r + lane;
-      if (row < q && row >= c) sm.L[row][c] = (row == c) ? dcc : s[r] / dcc;
-      if (row == c) rd[r] = 1.f / dcc;
-    }
-    wsync();
   }
 }
 
@@ -604,9 +557,11 @@ struct Sweep<NUM, R, NUM> {
 // (sg = -1, F -> A) pivot on k: a rank-1 update of the register rows, no factorization, and a
 // box-constrained solve of a guess A is one product with T (matvec_T).
 // The pivot row is broadcast through LDS with its entry k replaced by T_kk - sg, so the common
-// FMA leaves sg * T_ik / T_kk in column k of every other row. The pivot lane's own diagonal
-// entry then ends 2 sg away from -1/T_kk: the exact diagonal is carried in dg, and ed (a small
-// integer, exact in fp32) records the offset of the register copy, which matvec_T removes.
+// FMA leaves sg * T_ik / T_kk in column k of every other row. The pivot lane zeroes its own row
+// first, so the same FMA (f = -sg / T_kk) writes sg T_kj / T_kk there exactly (folding it in as
+// T_kj - (1 - sg / T_kk) T_kj cancels when |T_kk| >> 1: 5e-4 relative on stiff QPs); its
+// diagonal entry then ends sg away from -1/T_kk: the exact diagonal is carried in dg, and ed
+// (+-1 or 0, exact in fp32) records the offset of the register copy, which matvec_T removes.
 template <int NUM, bool GAP, int R>
 __device__ __forceinline__ void pivot_T(Smem<NUM, GAP>& sm, float (&h)[R][NUM], float (&dg)[R],
                                         float (&ed)[R], int lane, const int (&vv)[R], int k,
@@ -617,8 +572,10 @@ __device__ __forceinline__ void pivot_T(Smem<NUM, GAP>& sm, float (&h)[R][NUM], 
     for (int r = 0; r < R; r++) {
       if (r == kr) {
 #pragma unroll
-        for (int j = 0; j < NUM; j += 4)
+        for (int j = 0; j < NUM; j += 4) {
           *reinterpret_cast<f32x4*>(&sm.prow[j]) = f32x4{h[r][j], h[r][j + 1], h[r][j + 2], h[r][j + 3]};
+          h[r][j] = 0.f; h[r][j + 1] = 0.f; h[r][j + 2] = 0.f; h[r][j + 3] = 0.f;
+        }
         sm.prow[k] = dg[r] - sg;
       }
     }
@@ -637,7 +594,7 @@ __device__ __forceinline__ void pivot_T(Smem<NUM, GAP>& sm, float (&h)[R][NUM], 
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const bool piv = (r == kr) && (lane == kl);
-    const float f = piv ? fmaf(-sg, inv, 1.f) : tk[r] * inv;
+    const float f = piv ? -sg * inv : tk[r] * inv;  // pivot row zeroed above: sg T_kj / T_kk exactly
     const f32x2 nf = {-f, -f};
 #pragma unroll
     for (int j = 0; j < NUM; j += 2) {
@@ -647,7 +604,7 @@ __device__ __forceinline__ void pivot_T(Smem<NUM, GAP>& sm, float (&h)[R][NUM], 
       h[r][j + 1] = x.y;
     }
     dg[r] = piv ? -inv : fmaf(-f, tk[r], dg[r]);
-    ed[r] += piv ? 2.f * sg : 0.f;
+    ed[r] = piv ? sg : ed[r];  // register diagonal sg (T_kk - sg) / T_kk = sg - 1/T_kk
   }
   wsync();  // prow is rewritten by the next pivot
 }
@@ -680,29 +637,25 @@ __device__ __forceinline__ void matvec_T(Smem<NUM, GAP>& sm, const float (&h)[R]
   wsync();  // yb is rewritten by the next product
 }
 
-// Build the slots of the bound guess act (0 free, 1 lower, 2 upper) in variable order and
-// factor S_A. Returns the slot count.
-template <int NUM, bool GAP, int R>
-__device__ __forceinline__ int build_box_slots(Smem<NUM, GAP>& sm, int lane, const int (&act)[R],
-                                               int (&slot_id)[R], float (&rd)[R]) {
-  int base = 0;
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const unsigned long long mask = __ballot(act[r] != 0);
-    const int myslot = base + __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0));
-    if (act[r]) sm.ids[myslot] = 3 * (64 * r + lane) + (act[r] == 2 ? 1 : 0);
-    base += __popcll(mask);
-  }
-  wsync();
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const int s = 64 * r + lane;
-    slot_id[r] = (s < base) ? sm.ids[s] : -1;
-  }
-  chol_slots<NUM, GAP, R>(sm, lane, base, slot_id, rd);
-  return base;
-}
+// fp64 iterative refinement of the fp32 solve (steps 4a/5): each step evaluates the residual in
+// fp64 (rollout + adjoint) and corrects through the fp32 T / W. Stiff problems (large dt x N: H's
+// condition number grows like (N dt v)^2) contract more slowly per step; the fuzz test over the
+// ABI's range (dt 0.05, N = 40) needed more than the two steps that suffice at the shipped
+// dt = 0.01, so up to four, stopping once the fp32 correction is at its noise level.
+constexpr int kRefineSteps = 4;
+constexpr float kRefineTol = 2e-6f;
+// box path's fp64 PDAS (step 4a'): passes, HIK passes before the least-index rule, flips pivoted
+// in place before T is rebuilt, refinement steps and tolerance per pass
+constexpr int kHikPasses = 8;
+constexpr int kIncPivots = 8;
+constexpr int kRobSteps = 12;
+constexpr float kRobTol = 1e-9f;     // converged
+constexpr float kRobTight = 1e-14f;  // keep going to fp64 level: the multipliers r1_A = (Hu + g)_A
+                                     // carry ||H_AF|| times the error left in u_F
+template <int NUM>
+constexpr int kRobPasses = kHikPasses + NUM;
+// GI's final check: an active row's multiplier below -kMultTol (1 + max|g|) is a wrong set
+constexpr double kMultTol = 1e-4;
 
 template <int NUM, bool GAP>
 __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const KParams& P,
@@ -854,6 +807,65 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   STAMP(t_hess);
   STAMP(t_inv);
   float hrow[R][NUM];  // condensed Hessian rows, swept in place to T = -H^-1 (box path keeps it)
+  // ---- 2b. condensed Hessian rows (closed form, fp32) -------------------------------------
+  // Row v = (k, a), column w = (l, b). For l <= k the stages that see both inputs are
+  // i = k+1..N (T = N-k of them), and Gamma_i[:, w] is affine in the stage distance, so
+  //   H[v][w] = C0_b + C1_b * (k - l)
+  // with four per-row constants (sums of 1, t, t^2 over the T stages). The entries with
+  // l > k are the transpose: every lane publishes its lower rows and reads column v back.
+  // hd = the diagonal of this lane's rows (the exact pivot values pivot_T carries). Also
+  // rebuilt by the box path's fp64 PDAS for a fresh T (step 4a').
+  auto build_H = [&](float (&hd)[R]) __attribute__((always_inline)) {
+    // The row constants and entries are formed in fp64 and rounded once: in fp32 the sums
+    // C0 + C1 (k - l) cancel (|C1 (k - l)| ~ 1e5 against entries ~ 1) and on stiff QPs
+    // (kappa(H) ~ 4e5 at N = 48, dt = 0.05) that error alone made -H^-1 a divergent
+    // preconditioner for the fp64 refinement; correctly rounded entries keep it at ~1e-3.
+    const Lin M = sm.M;
+    const double q0 = P.q[0], q1 = P.q[1], q2 = P.q[2];
+    const double ra = a ? P.r[1] : P.r[0];
+    const double beta_a = a ? M.b21 : M.b20;
+    const double pxa = a ? 0.0 : M.b00, pya = a ? 0.0 : M.b10;  // dk = 0 in this regime
+    const double sxa = M.a02 * beta_a, sya = M.a12 * beta_a;
+    double C0[R][2], C1[R][2];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const double T = (double)(N - kk[r]);
+      const double S1 = T * (T - 1.0) * 0.5;
+      const double S2 = (T - 1.0) * T * (2.0 * T - 1.0) * (1.0 / 6.0);
+      const double Ux = T * pxa + sxa * S1, Vx = pxa * S1 + sxa * S2;
+      const double Uy = T * pya + sya * S1, Vy = pya * S1 + sya * S2;
+#pragma unroll
+      for (int bb = 0; bb < 2; bb++) {
+        const double beta_b = bb ? M.b21 : M.b20;
+        const double ax_b = bb ? 0.0 : M.b00, ay_b = bb ? 0.0 : M.b10;
+        const double sxb = M.a02 * beta_b, syb = M.a12 * beta_b;
+        C0[r][bb] = q0 * (ax_b * Ux + sxb * Vx) + q1 * (ay_b * Uy + syb * Vy) + q2 * T * beta_a * beta_b;
+        C1[r][bb] = q0 * sxb * Ux + q1 * syb * Uy;
+      }
+      if (vv[r] < NUM) {
+#pragma unroll
+        for (int w = 0; w < NUM; w++) {
+          const int l = w >> 1, bb = w & 1;  // exchange via L: row stride NUM + 1, conflict-free
+          sm.L[vv[r]][w] = (float)fma(C1[r][bb], (double)(kk[r] - l), C0[r][bb]);
+        }
+      }
+    }
+    wsync();
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+#pragma unroll
+      for (int w = 0; w < NUM; w++) {
+        const int l = w >> 1, bb = w & 1;
+        float h;
+        if (w == vv[r]) h = (float)(C0[r][bb] + ra);
+        else h = (l <= kk[r]) ? (float)fma(C1[r][bb], (double)(kk[r] - l), C0[r][bb]) : sm.L[w][cl[r]];
+        const bool ok = valid[r] && (w < NU);
+        hrow[r][w] = ok ? h : (w == vv[r] ? 1.f : 0.f);
+      }
+      hd[r] = vv[r] < NUM ? (valid[r] ? (float)((a ? C0[r][1] : C0[r][0]) + ra) : 1.f) : 0.f;
+    }
+    wsync();
+  };
   if (whit) {
     // ---- 2b/3 (cache hit): W from the slot / group cache, no Hessian, no sweep ----------
     const float* Wc = ws.W + (size_t)wslot * NU * NU;
@@ -873,59 +885,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #pragma unroll
       for (int j = 0; j < NUM; j++) hrow[r][j] = (vv[r] < NUM) ? -sm.W[j][vv[r]] : 0.f;
   } else {
-  // ---- 2b. condensed Hessian rows (closed form, fp32) -------------------------------------
-  // Row v = (k, a), column w = (l, b). For l <= k the stages that see both inputs are
-  // i = k+1..N (T = N-k of them), and Gamma_i[:, w] is affine in the stage distance, so
-  //   H[v][w] = C0_b + C1_b * (k - l)
-  // with four per-row constants (sums of 1, t, t^2 over the T stages). The entries with
-  // l > k are the transpose: every lane publishes its lower rows and reads column v back.
-  {
-    const Lin M = sm.M;
-    const float fa02 = (float)M.a02, fa12 = (float)M.a12, fb00 = (float)M.b00;
-    const float fb10 = (float)M.b10, fb20 = (float)M.b20, fb21 = (float)M.b21;
-    const float q0 = (float)P.q[0], q1 = (float)P.q[1], q2 = (float)P.q[2];
-    const float ra = a ? (float)P.r[1] : (float)P.r[0];
-    const float beta_a = a ? fb21 : fb20;
-    const float pxa = a ? 0.f : fb00, pya = a ? 0.f : fb10;  // dk = 0 in this regime
-    const float sxa = fa02 * beta_a, sya = fa12 * beta_a;
-    float C0[R][2], C1[R][2];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const float T = (float)(N - kk[r]);
-      const float S1 = T * (T - 1.f) * 0.5f;
-      const float S2 = (T - 1.f) * T * (2.f * T - 1.f) * (1.f / 6.f);
-      const float Ux = T * pxa + sxa * S1, Vx = pxa * S1 + sxa * S2;
-      const float Uy = T * pya + sya * S1, Vy = pya * S1 + sya * S2;
-#pragma unroll
-      for (int bb = 0; bb < 2; bb++) {
-        const float beta_b = bb ? fb21 : fb20;
-        const float ax_b = bb ? 0.f : fb00, ay_b = bb ? 0.f : fb10;
-        const float sxb = fa02 * beta_b, syb = fa12 * beta_b;
-        C0[r][bb] = q0 * (ax_b * Ux + sxb * Vx) + q1 * (ay_b * Uy + syb * Vy) + q2 * T * beta_a * beta_b;
-        C1[r][bb] = q0 * sxb * Ux + q1 * syb * Uy;
-      }
-      if (vv[r] < NUM) {
-#pragma unroll
-        for (int w = 0; w < NUM; w++) {
-          const int l = w >> 1, bb = w & 1;  // exchange via L: row stride NUM + 1, conflict-free
-          sm.L[vv[r]][w] = fmaf(C1[r][bb], (float)(kk[r] - l), C0[r][bb]);
-        }
-      }
-    }
-    wsync();
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-#pragma unroll
-      for (int w = 0; w < NUM; w++) {
-        const int l = w >> 1, bb = w & 1;
-        float h = (l <= kk[r]) ? fmaf(C1[r][bb], (float)(kk[r] - l), C0[r][bb]) : sm.L[w][cl[r]];
-        if (w == vv[r]) h += ra;
-        const bool ok = valid[r] && (w < NU);
-        hrow[r][w] = ok ? h : (w == vv[r] ? 1.f : 0.f);
-      }
-    }
-    wsync();
-  }
+  float hd[R];
+  build_H(hd);
   if (Hdbg) {  // debug/parity hook: dump H and g, no solve
     inputs_and_gradient();
 #pragma unroll
@@ -940,7 +901,35 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   }
   STAMP_SET(t_hess);
   // ---- 3. W = H^-1 : symmetric sweep (Goodnight), rows in registers -----------------------
-  Sweep<NUM, R, 0>::run(hrow, lane);
+  // Jacobi scaling around the sweep: sweep D H D (unit diagonal, every later pivot <= 1) and
+  // scale back, W = D (D H D)^-1 D. The sweep folds the pivot row's update into the common FMA
+  // (f = 1 - 1/a_pp), which loses ~eps |a_pp| of that row relative; with pivots <= 1 nothing
+  // cancels. Unscaled, stiff QPs (H_kk ~ 8e3 at N = 48, dt = 0.05) got W rows 5e-4 off and the
+  // fp64 refinement through W contracted by only 0.25 per step.
+  {
+    float dsc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      dsc[r] = (vv[r] < NUM && hd[r] > 0.f) ? __builtin_amdgcn_rsqf(hd[r]) : 1.f;
+      if (vv[r] < NUM) sm.yb[vv[r]] = dsc[r];
+    }
+    wsync();
+    auto scale_rows = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < NUM; j += 4) {
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&sm.yb[j]);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          hrow[r][j] *= dsc[r] * d4.x; hrow[r][j + 1] *= dsc[r] * d4.y;
+          hrow[r][j + 2] *= dsc[r] * d4.z; hrow[r][j + 3] *= dsc[r] * d4.w;
+        }
+      }
+    };
+    scale_rows();
+    Sweep<NUM, R, 0>::run(hrow, lane);
+    scale_rows();
+    wsync();
+  }
 #pragma unroll
   for (int r = 0; r < R; r++) {
     if (vv[r] < NUM) {
@@ -1045,24 +1034,164 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   bool gi_start = true;  // GI starts from the unconstrained point (x = -W g)
   int forced_p = -1;     // violated row found by the fp64 re-check
   float forced_sp = 0.f;
+  bool inexact = false;  // GI's final check failed: SOLVED_INACCURATE
+  float gmax = 0.f;      // max |g| (scale of the multiplier tolerances)
+#pragma unroll
+  for (int r = 0; r < R; r++) gmax = fmaxf(gmax, valid[r] ? fabsf(sm.vec[vv[r]]) : 0.f);
+  {
+    int dummy = 0;
+    gmax = -gmax;
+    wave_argmin(gmax, dummy);
+    gmax = -gmax;
+  }
+
+  // ---- box rows: fp64 machinery of steps 4a' and 6 (T, its set, the fp64 point) ----------
+  float dg[R], ed[R];   // exact diagonal of T / offset of its register copy (pivot_T)
+  int act[R], nact[R];  // 0 free, 1 at the lower bound, 2 at the upper bound
+#pragma unroll
+  for (int r = 0; r < R; r++) { dg[r] = 0.f; ed[r] = 0.f; act[r] = 0; nact[r] = 0; }
+  // r1 = H u + g at u64 (fp64 rollout and costate); the references are re-read from LDS so
+  // that nothing of this rare path stays live across the fp32 loop above
+  auto residual = [&](double (&r1)[R]) __attribute__((always_inline)) {
+    const Lin M = sm.M;
+    double rxd[R], ryd[R], rthd[R], zero[R], px[R], py[R], th[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      rxd[r] = sm.rx[vv[r]]; ryd[r] = sm.ry[vv[r]]; rthd[r] = sm.rth[vv[r]];
+      zero[r] = 0.0;
+    }
+    rollout_f64<R>(M, lane, u64, px, py, th);
+    grad_f64<R>(M, P, lane, N, u64, px, py, th, rxd, ryd, rthd, zero, zero, r1);
+  };
+  // u_F += T_FF r1_F (r1 = H u + g in fp64) until max |du| <= tight; converged if <= loose
+  // (past `steps`, up to steps_max while each step still halves the correction). Converged:
+  // the last correction <= loose and the error it leaves, ~ |du|^2 / |du_prev| at the observed
+  // contraction, <= 1e-8: a slowly contracting T (stiff QP) keeps refining instead of stopping
+  // at a 2e-6 step that still leaves ~1e-6 in u.
+  auto refine = [&](int steps, float tight, float loose, int steps_max) __attribute__((always_inline)) -> bool {
+    float adx = 3.0e38f, prev = 3.0e38f;
+    bool conv = false;
+    for (int rs = 0; rs < steps_max; rs++) {
+      double r1[R];
+      residual(r1);
+      float y[R], dx[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) y[r] = (valid[r] && !act[r]) ? (float)r1[r] : 0.f;
+      matvec_T<NUM, GAP, R>(sm, hrow, ed, vv, y, dx);
+      float mx = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const bool fr = valid[r] && !act[r];
+        if (fr) u64[r] += (double)dx[r];
+        const float m = fr ? fabsf(dx[r]) : 0.f;
+        mx = fmaxf(mx, (m == m) ? m : 3.0e38f);  // a NaN correction never converges
+      }
+      int dummy = 0;
+      mx = -mx;
+      wave_argmin(mx, dummy);  // -max |dx|
+      adx = -mx;
+      conv = adx <= loose && adx * adx <= 1e-8f * prev;
+      if (adx <= tight && conv) break;
+      if (rs + 1 >= steps && !(adx < 0.5f * prev)) break;
+      prev = adx;
+    }
+    return conv;
+  };
+  // T for the current set from H: forward sweeps of the free variables only
+  // (Jacobi-scaled like the full sweep: T^ = SWP_F(D H D) has T_FF = D T^_FF D, T_FA = D T^_FA
+  // D^-1, T_AA = D^-1 T^_AA D^-1, i.e. entry (i, j) times s_i s_j with s = d on F, 1/d on A.
+  // Unscaled, fp32 elimination of the stiff H (entries ~8e3, lambda_min ~0.4) left T_FF 10% off
+  // and the refinement through it diverged.)
+  auto fresh_T = [&]() __attribute__((always_inline)) {
+    build_H(dg);
+    float dsc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      ed[r] = 0.f;
+      dsc[r] = (vv[r] < NUM && dg[r] > 0.f) ? __builtin_amdgcn_rsqf(dg[r]) : 1.f;
+      if (vv[r] < NUM) sm.yb[vv[r]] = dsc[r];
+    }
+    wsync();
+    auto scale = [&]() __attribute__((always_inline)) {  // h_ij *= s_i s_j from sm.yb
+#pragma unroll
+      for (int j = 0; j < NUM; j += 4) {
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&sm.yb[j]);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const float si = sm.yb[vv[r] < NUM ? vv[r] : 0];
+          hrow[r][j] *= si * d4.x; hrow[r][j + 1] *= si * d4.y;
+          hrow[r][j + 2] *= si * d4.z; hrow[r][j + 3] *= si * d4.w;
+        }
+      }
+    };
+    scale();
+#pragma unroll
+    for (int r = 0; r < R; r++) dg[r] *= dsc[r] * dsc[r];
+#pragma unroll
+    for (int r0 = 0; r0 < R; r0++) {
+      unsigned long long m = __ballot(valid[r0] && act[r0] == 0);
+      while (m) {
+        const int bit = __builtin_ctzll(m);
+        m &= m - 1;
+        pivot_T<NUM, GAP, R>(sm, hrow, dg, ed, lane, vv, 64 * r0 + bit, 1.f);
+      }
+    }
+    float s[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      s[r] = (valid[r] && act[r]) ? 1.f / dsc[r] : dsc[r];
+      if (vv[r] < NUM) sm.yb[vv[r]] = s[r];
+    }
+    wsync();
+    scale();
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      dg[r] *= s[r] * s[r];
+      ed[r] *= s[r] * s[r];
+    }
+    wsync();
+  };
+  // exact KKT re-check at u64: nact = act with every violator flipped; any violation?
+  // Both tests in primal units: a free variable past its bound by more than 1e-9 (1 + |b|),
+  // an active one whose wrong-sign multiplier would move it by more than that once freed
+  // (|r1| / T_ii, T_ii = the Schur complement H_ii - H_iF H_FF^-1 H_Fi carried in dg): a
+  // multiplier tolerance in gradient units let a near-degenerate bound of a stiff QP stay
+  // active with an error of |r1| / curvature ~ 1e-3 in u.
+  auto kkt_violated = [&]() __attribute__((always_inline)) -> bool {
+    double r1f[R];
+    residual(r1f);
+    bool any = false;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      nact[r] = act[r];
+      if (!valid[r]) continue;
+      if (act[r]) {
+        const double bnd = act[r] == 1 ? (double)lb[r] : (double)ub[r];
+        const double lam = act[r] == 1 ? r1f[r] : -r1f[r];  // >= 0 at the optimum
+        if (!(lam >= -1e-9 * (1.0 + fabs(bnd)) * fmax((double)dg[r], 0.0))) nact[r] = 0;
+      } else {
+        const double s0 = (u64[r] - (double)lb[r]) / (1.0 + fabs((double)lb[r]));
+        const double s1 = ((double)ub[r] - u64[r]) / (1.0 + fabs((double)ub[r]));
+        nact[r] = s0 < -1e-9 ? 1 : (s1 < -1e-9 ? 2 : 0);
+      }
+      any = any || (nact[r] != act[r]);
+    }
+    return __ballot(any) != 0ull;
+  };
 
   // ---- 4a. box rows only: primal-dual active set (Hintermueller-Ito-Kunisch) on T ----------
   // Each pass solves the equality QP of the current guess A with one product x = T y
   // (y = g on F, -bound on A): u_F = x_F, and the bound multipliers are lambda_A = g_A - x_A
   // (lambda = Hu + g). The next guess follows from the multipliers and the bounds; each
   // variable that enters or leaves A is one pivot of T. On these QPs the optimal set is
-  // reached in <= 5 passes. The fixed point is then refined in fp64 (residual from the fp64
-  // rollout and costate, correction through T on F) and re-checked exactly; a violated row
-  // hands the set over to the GI loop below as a valid GI state (independent normals,
-  // positive multipliers). No convergence within P.pdas_max passes (10) -> plain GI from the
-  // unconstrained point. (Measured and not kept for the gap-row kernel: the same box PDAS first,
+  // reached in <= 5 passes (P.pdas_max = 10); step 4a' then refines and certifies it in fp64.
+  // (Measured and not kept for the gap-row kernel: the same box PDAS first,
   // then GI from its set for the violated gap rows: C3 327 -> 451 us, the GI steps are the gap
   // rows themselves and the extra code halves that kernel's occupancy.)
   if constexpr (!GAP) {
     if (status == F110QP_SOLVED_ID) {
       STAMP(t_pdas);
-      float dg[R], ed[R], gr[R], u[R], lam[R];
-      int act[R];  // 0 free, 1 at the lower bound, 2 at the upper bound
+      float gr[R], u[R], lam[R];
 #pragma unroll
       for (int r = 0; r < R; r++) {
         dg[r] = (vv[r] < NUM) ? -sm.W[vv[r]][vv[r]] : 0.f;
@@ -1123,105 +1252,92 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #pragma unroll
         for (int r = 0; r < R; r++) act[r] = nact[r];
       }
+      if (!converged) it = P.pdas_max;
       STAMP_ACC(acc_pdas, t_pdas);
-      if (converged) {
-        STAMP(t_ref0);
-        // fp64 refinement: r1 = Hu + g on F from the fp64 rollout and costate, du_F = T_FF r1_F
-        const Lin M = sm.M;
-        double rxd[R], ryd[R], rthd[R], zero[R], px[R], py[R], th[R];
+      // ---- 4a'. acceptance in fp64, and the fp64 PDAS behind it ----------------------------
+      // The fp32 fixed point is refined in fp64 (residual from the fp64 rollout and costate,
+      // correction through T on F) and accepted only if the refinement converged and the exact
+      // re-check holds: every free variable inside its box, every active bound's multiplier
+      // r1 = (H u + g)_A of the right sign (lower: r1 >= 0, upper: r1 <= 0). Otherwise the same
+      // PDAS continues on the fp64 values: HIK updates (every violator flips) for kHikPasses
+      // passes, then one flip per pass, the least-index violator (Murty's rule, finite for SPD H),
+      // each pass's equality solve refined to kRobTol. A few flips pivot T in place; more, or a
+      // refinement that stalls, rebuild T from H by forward sweeps of the free set only: reverse
+      // sweeps out of the full inverse lose T's accuracy on stiff H (condition number ~ (N dt v)^2:
+      // 4e5 at N = 48, dt = 0.05, where the fp32 set of a bang-bang optimum, 95 of 96 bounds
+      // active, was wrong or its refinement stalled). No fixed point within kRobPasses -> GI from
+      // the unconstrained point, whose own final check reports SOLVED_INACCURATE, never a wrong
+      // SOLVED.
+      STAMP(t_ref0);
+      {
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-          rxd[r] = sm.rx[vv[r]]; ryd[r] = sm.ry[vv[r]]; rthd[r] = sm.rth[vv[r]];
-          zero[r] = 0.0;
-          u64[r] = valid[r] ? (double)u[r] : 0.0;  // active entries are the bounds exactly
-        }
-        for (int rs = 0; rs < 2; rs++) {
-          double r1[R];
-          rollout_f64<R>(M, lane, u64, px, py, th);
-          grad_f64<R>(M, P, lane, N, u64, px, py, th, rxd, ryd, rthd, zero, zero, r1);
-          float y[R], dx[R];
+        for (int r = 0; r < R; r++)
+          u64[r] = !valid[r] ? 0.0 : (act[r] == 1 ? (double)lb[r] : (act[r] == 2 ? (double)ub[r] : (double)u[r]));
+        bool ref_ok = converged && refine(kRefineSteps, kRefineTol, kRefineTol, kRobSteps);
+        bool fresh = false, accept = false;
+        int pass = 0;
+        for (;;) {
+          if (ref_ok && !kkt_violated()) { accept = true; break; }
+          if (pass >= kRobPasses<NUM> || it >= max_iter) break;
+          if (!ref_ok) {
+            if (fresh) break;  // a fresh T stalls too
+            fresh_T();
+            fresh = true;
+          } else {
+            if (pass >= kHikPasses) {  // least-index violator only
+              int first = 0x7fffffff;
 #pragma unroll
-          for (int r = 0; r < R; r++) y[r] = (valid[r] && !act[r]) ? (float)r1[r] : 0.f;
-          matvec_T<NUM, GAP, R>(sm, hrow, ed, vv, y, dx);
-          float adx = 0.f;
+              for (int r0 = R - 1; r0 >= 0; r0--) {
+                const unsigned long long m = __ballot(nact[r0] != act[r0]);
+                if (m) first = 64 * r0 + __builtin_ctzll(m);
+              }
 #pragma unroll
-          for (int r = 0; r < R; r++) {
-            const bool fr = valid[r] && !act[r];
-            if (fr) u64[r] += (double)dx[r];
-            adx = fmaxf(adx, fr ? fabsf(dx[r]) : 0.f);
+              for (int r = 0; r < R; r++)
+                if (vv[r] != first) nact[r] = act[r];
+            }
+            int nchg = 0;
+#pragma unroll
+            for (int r0 = 0; r0 < R; r0++) nchg += __popcll(__ballot(nact[r0] != act[r0]));
+            if (nchg > kIncPivots) {
+#pragma unroll
+              for (int r = 0; r < R; r++) act[r] = nact[r];
+              fresh_T();
+              fresh = true;
+            } else {
+#pragma unroll
+              for (int r0 = 0; r0 < R; r0++) {
+                unsigned long long enter = __ballot(act[r0] == 0 && nact[r0] != 0);
+                unsigned long long leave = __ballot(act[r0] != 0 && nact[r0] == 0);
+                while (enter) {
+                  const int bit = __builtin_ctzll(enter);
+                  enter &= enter - 1;
+                  pivot_T<NUM, GAP, R>(sm, hrow, dg, ed, lane, vv, 64 * r0 + bit, -1.f);
+                }
+                while (leave) {
+                  const int bit = __builtin_ctzll(leave);
+                  leave &= leave - 1;
+                  pivot_T<NUM, GAP, R>(sm, hrow, dg, ed, lane, vv, 64 * r0 + bit, 1.f);
+                }
+              }
+#pragma unroll
+              for (int r = 0; r < R; r++) act[r] = nact[r];
+              fresh = false;
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++)
+              if (valid[r]) u64[r] = act[r] == 1 ? (double)lb[r] : (act[r] == 2 ? (double)ub[r] : u64[r]);
+            pass++;
+            it++;
           }
-          int dummy = 0;
-          adx = -adx;
-          wave_argmin(adx, dummy);  // -max |dx|
-          if (-adx <= 1e-5f) break;
+          ref_ok = refine(3, kRobTight, kRobTol, kRobSteps);
         }
-        // exact re-check at the refined point, in fp64: the box rows of the free variables and
-        // the sign of the active bounds' multipliers r1 = (H u + g)_A (lower bound: r1 >= 0,
-        // upper: r1 <= 0; the fp32 PDAS decided them)
-        double r1f[R];
-        rollout_f64<R>(M, lane, u64, px, py, th);
-        grad_f64<R>(M, P, lane, N, u64, px, py, th, rxd, ryd, rthd, zero, zero, r1f);
-        float gmax = 0.f;
-#pragma unroll
-        for (int r = 0; r < R; r++) gmax = fmaxf(gmax, valid[r] ? fabsf(gr[r]) : 0.f);
-        {
-          int dummy = 0;
-          gmax = -gmax;
-          wave_argmin(gmax, dummy);
-          gmax = -gmax;
-        }
-        const double dtol = 1e-6 * (1.0 + (double)gmax);
-        bool dual_bad = false;
-        float best64 = 0.f, sp64 = 0.f;
-        int bid64 = 0x7fffffff;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-          if (!valid[r]) continue;
-          const int v = vv[r];
-          if (act[r] == 1 && r1f[r] < -dtol) dual_bad = true;
-          if (act[r] == 2 && r1f[r] > dtol) dual_bad = true;
-          if (act[r]) continue;
-          const double s0 = u64[r] - (double)lb[r], s1 = (double)ub[r] - u64[r];
-          const float v0 = (float)(s0 / (1.0 + fabs((double)lb[r])));
-          const float v1 = (float)(s1 / (1.0 + fabs((double)ub[r])));
-          if (v0 < -1e-9f && v0 < best64) { best64 = v0; bid64 = 3 * v; sp64 = (float)s0; }
-          if (v1 < -1e-9f && v1 < best64) { best64 = v1; bid64 = 3 * v + 1; sp64 = (float)s1; }
-        }
-        wave_argmin(best64, bid64);
-        dual_bad = __ballot(dual_bad) != 0ull;
-#pragma unroll
-        for (int r = 0; r < R; r++) actf[r] = act[r];  // bit0 lower, bit1 upper
         STAMP_ACC(acc_refine, t_ref0);
-        if (dual_bad) {
-          // a wrong-sign multiplier: the set is not optimal; plain GI from the unconstrained point
-#pragma unroll
-          for (int r = 0; r < R; r++) actf[r] = 0;
-        } else if (bid64 == 0x7fffffff) {
+        if (accept) {
           final_ok = true;
-        } else {
-          // hand the set to the GI state: slots, chol(S_A), multipliers, the violated row
-          int sid[R];
-          float rdp[R];
-          q = build_box_slots<NUM, GAP, R>(sm, lane, act, sid, rdp);
 #pragma unroll
-          for (int r = 0; r < R; r++) {
-            if (valid[r]) sm.pmu[vv[r]] = act[r] == 1 ? lam[r] : -lam[r];
-            xv[r] = valid[r] ? (float)u64[r] : 0.f;
-          }
-          wsync();
-#pragma unroll
-          for (int r = 0; r < R; r++) {
-            const bool sl = 64 * r + lane < q;
-            slot_id[r] = sl ? sid[r] : -1;
-            mult[r] = sl ? fmaxf(sm.pmu[sid[r] / 3], 0.f) : 0.f;
-            rdiag[r] = sl ? rdp[r] : 0.f;
-          }
-          reentries = 1;
-          forced_p = bid64;
-          forced_sp = readlane_f(sp64, (bid64 / 3) & 63);
-          gi_start = false;
-          wsync();
+          for (int r = 0; r < R; r++) actf[r] = act[r];  // bit0 lower, bit1 upper
         }
+        // else: GI from the unconstrained point (gi_start)
       }
     }
   }
@@ -1235,6 +1351,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     for (int r = 0; r < R; r++) actf[r] = 0;
   }
 
+  const bool gi_fallback = !final_ok && status == F110QP_SOLVED_ID;  // box rows: behind the fp64 PDAS
   // ---- 4b. dual active set (Goldfarb-Idnani, range space) ---------------------------------
   while (status == F110QP_SOLVED_ID && !final_ok) {
     // ---- step 1: most violated inactive constraint (fp32, scaled) ----
@@ -1291,7 +1408,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #pragma unroll
         for (int r = 0; r < R; r++) { rxd[r] = sm.rx[vv[r]]; ryd[r] = sm.ry[vv[r]]; rthd[r] = sm.rth[vv[r]]; }
         double px[R], py[R], th[R];
-        for (int rs = 0; rs < 2; rs++) {
+        bool gi_ref_ok = false;
+        for (int rs = 0; rs < kRefineSteps; rs++) {
           wsync();
           rollout_f64<R>(M, lane, u64, px, py, th);
           double gmx[R], gmy[R];  // gap multipliers of the variable's stage (sides 0,1)
@@ -1378,7 +1496,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           int dummy = 0;
           adx = -adx;
           wave_argmin(adx, dummy);  // -max |dx|
-          if (-adx <= 1e-5f) break;
+          if (-adx <= kRefineTol) { gi_ref_ok = true; break; }
         }
         wsync();
         // fp64 feasibility check of every inactive row at the refined point
@@ -1404,6 +1522,14 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         wave_argmin(best64, bid64);
         STAMP_ACC(acc_refine, t_ref0);
         if (bid64 == 0x7fffffff || reentries >= 4) {
+          // final check: the refinement converged, no row violated, no multiplier of the wrong
+          // sign; otherwise the point is reported as SOLVED_INACCURATE
+          float mneg = 0.f;
+#pragma unroll
+          for (int r = 0; r < R; r++) mneg = fminf(mneg, (64 * r + lane < q) ? mult[r] : 0.f);
+          int dummy = 0;
+          wave_argmin(mneg, dummy);
+          inexact = !gi_ref_ok || bid64 != 0x7fffffff || !((double)mneg >= -kMultTol * (1.0 + (double)gmax));
           final_ok = true;
           break;
         }
@@ -1590,9 +1716,23 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   }
 
   STAMP(t_gi);
+  if constexpr (!GAP) {
+    // box rows: GI's point is certified like the PDAS one, in fp64 (its set, a fresh T, the
+    // refined point, the exact KKT check); and a box (u_min <= u_max, checked at create) is never
+    // empty, so GI's infeasibility there is a numerical breakdown
+    if (gi_fallback && final_ok && status == F110QP_SOLVED_ID) {
+#pragma unroll
+      for (int r = 0; r < R; r++) act[r] = (actf[r] & 1) ? 1 : ((actf[r] & 2) ? 2 : 0);
+      fresh_T();
+      const bool conv = refine(3, kRobTight, kRobTol, kRobSteps);
+      inexact = !conv || kkt_violated();
+    }
+    if (gi_fallback && status == F110QP_PRIMAL_INFEASIBLE_ID) status = F110QP_NUMERICAL_ID;
+  }
   // ---- 6. outputs ---------------------------------------------------------------------------
   if (status == F110QP_SOLVED_ID && !final_ok) status = F110QP_MAX_ITER_ID;
-  const bool ok = (status == F110QP_SOLVED_ID);
+  if (status == F110QP_SOLVED_ID && inexact) status = F110QP_SOLVED_INACCURATE_ID;
+  const bool ok = (status == F110QP_SOLVED_ID) || (status == F110QP_SOLVED_INACCURATE_ID);
   {
     double uo[R], px[R], py[R], th[R];
 #pragma unroll

@@ -20,6 +20,7 @@ ERR_INVALID = -1
 ERR_HIP = -2
 ERR_ALLOC = -3
 SOLVED = 1
+SOLVED_INACCURATE = 2
 MAX_ITER = -2
 PRIMAL_INFEASIBLE = -3
 NUMERICAL = -10

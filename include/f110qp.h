@@ -66,6 +66,8 @@ extern "C" {
 
 /* per-QP status codes (values follow OSQP's status ids) */
 #define F110QP_SOLVED 1
+#define F110QP_SOLVED_INACCURATE 2 /* wave back end: a point whose fp64 KKT check failed (u, x    */
+                                  /* written, not selected); see DESIGN.md, stiff problems     */
 #define F110QP_MAX_ITER -2
 #define F110QP_PRIMAL_INFEASIBLE -3
 #define F110QP_NUMERICAL -10      /* non-finite data or factorisation breakdown */

@@ -446,7 +446,9 @@ static int gi_solve(const double* H, const double* g, const double* Cn, const do
       double t1 = INFINITY; int k = -1;
       for (int a = 0; a < s.q; a++)
         if (r[a] > 0) { double tt = s.mult[a] / r[a]; if (tt < t1) { t1 = tt; k = a; } }
-      double t2 = (piv > 1e-12 * nw) ? -sp / piv : INFINITY;
+      /* with n independent rows active the point is fixed: a further row is dependent (a pivot
+         above the threshold there is rounding; adding it would overrun the n-slot state) */
+      double t2 = (s.q < n && piv > 1e-12 * nw) ? -sp / piv : INFINITY;
       double t = t1 < t2 ? t1 : t2;
       if (!isfinite(t)) { status = F110O_PRIMAL_INFEASIBLE; goto done; }
       for (int a = 0; a < s.q; a++) s.mult[a] -= t * r[a];
@@ -498,6 +500,18 @@ int f110o_solve(const f110o_params* prm, const double x0[3], const double ulin[2
   int q = 0, status;
   /* the stage-0 gap rows are constant (x0 lies on both lines, constraints.cpp:233-246): check */
   status = gi_solve(c.H, c.g, c.Cn, c.b, nu, c.m, uu, act, mult, &q);
+  if (status == F110O_SOLVED) {
+    /* self-check: every condensed row holds at the returned point. Near-infeasible gap wedges
+       with u_des on a bound drive the active set to n rows; GI's steps there are rounding and
+       have returned points 0.6 outside the box. Such a point is not a certificate. */
+    double xs = 0;
+    for (int k = 0; k < nu; k++) xs = fmax(xs, fabs(uu[k]));
+    for (int j = 0; j < c.m; j++) {
+      double t = -c.b[j];
+      for (int k = 0; k < nu; k++) t += c.Cn[(size_t)j * nu + k] * uu[k];
+      if (t < -1e-9 * (1.0 + fabs(c.b[j]) + xs)) { status = F110O_UNCERTIFIED; break; }
+    }
+  }
   if (gap_active && hs) {
     for (int h = 0; h < 2; h++)
       if (hs[3 * h] * x0[0] + hs[3 * h + 1] * x0[1] < -hs[3 * h + 2] - 1e-9) status = F110O_PRIMAL_INFEASIBLE;

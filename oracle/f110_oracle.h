@@ -29,6 +29,7 @@ extern "C" {
 #define F110O_SOLVED 1
 #define F110O_PRIMAL_INFEASIBLE -3
 #define F110O_MAX_ITER -2
+#define F110O_UNCERTIFIED -99 /* GI ended on a point that fails its own feasibility re-check */
 
 typedef struct {
   int horizon;        /* params.yaml:12 (reference default 30) */

@@ -29,6 +29,7 @@ LIB_PATH = os.path.join(HERE, "lib", "liboracle.so")
 SOLVED = 1
 MAX_ITER = -2
 PRIMAL_INFEASIBLE = -3
+UNCERTIFIED = -99  # the oracle's own re-check failed: no reference answer for this QP
 INFTY = 1e30
 
 

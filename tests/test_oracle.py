@@ -136,6 +136,59 @@ def test_exact_solve_vs_independent_bvls(oracle, N, seed):
         np.testing.assert_allclose(r["u"], ub, atol=1e-8)
 
 
+def _independent_gap_solve(oracle, prm, x0, ul, xr, hs):
+    """scipy SLSQP on the condensed form of the assembled sparse QP WITH its gap rows (C3
+    semantic): the dynamics rows eliminated from the CSC of oracle.assemble, the box and gap rows
+    as linear inequalities on u. No oracle solver code; SLSQP converged to 1e-12 in the objective."""
+    from scipy.optimize import minimize
+
+    N = prm.horizon
+    ns, n, m = 3 * (N + 1), 5 * N + 3, 7 * N + 5
+    d = oracle.assemble(prm, x0, ul, xr, hs, True)
+    P = _dense(d["P_colptr"], d["P_rowind"], d["P_val"], n, n)
+    A = _dense(d["A_colptr"], d["A_rowind"], d["A_val"], m, n)
+    E = A[:ns]
+    Ex, Eu = E[:, :ns], E[:, ns:]
+    G = -np.linalg.solve(Ex, Eu)
+    f = np.linalg.solve(Ex, d["l"][:ns])
+    Z = np.vstack([G, np.eye(2 * N)])
+    z0 = np.r_[f, np.zeros(2 * N)]
+    H = Z.T @ P @ Z
+    g = Z.T @ (P @ z0 + d["q"])
+    Ar, lo, hi = A[ns:] @ Z, d["l"][ns:] - A[ns:] @ z0, d["u"][ns:] - A[ns:] @ z0
+    fin_lo, fin_hi = lo > -1e29, hi < 1e29
+    cons = [{"type": "ineq", "fun": lambda u, M=Ar[fin_lo], c=lo[fin_lo]: M @ u - c, "jac": lambda u, M=Ar[fin_lo]: M},
+            {"type": "ineq", "fun": lambda u, M=Ar[fin_hi], c=hi[fin_hi]: c - M @ u, "jac": lambda u, M=Ar[fin_hi]: -M}]
+    u0 = np.clip(np.linalg.solve(H, -g), np.tile([3.0, -0.43], N), np.tile([4.5, 0.43], N))
+    res = minimize(lambda u: 0.5 * u @ H @ u + g @ u, u0, jac=lambda u: H @ u + g, constraints=cons,
+                   method="SLSQP", options={"ftol": 1e-14, "maxiter": 1000})
+    assert res.success, res.message
+    return res.x.reshape(N, 2)
+
+
+def test_exact_gap_solve_vs_independent_slsqp(oracle):
+    """The oracle's exact solve of the gap-row QP (C3 semantic) against an independent general
+    QP solve (scipy SLSQP) of the reference's own assembled sparse QP: the two agree to 1e-6
+    (SLSQP's accuracy), on instances with active gap rows."""
+    N = 20
+    prm = oracle.params(N)
+    B = 24
+    w = workload.make_batch(B, N, seed=1000)
+    ranges, amin, ainc, amax = workload.make_scans(B, seed=2000)
+    active = 0
+    for b in range(B):
+        rc, l1, l2, _, _ = oracle.find_half_spaces(w["x0"][b], ranges[b], amin, ainc, amax)
+        hs = np.array([l1, l2])
+        r = oracle.solve(prm, w["x0"][b], w["u_lin"][b], w["x_ref"][b], hs, True)
+        assert r["status"] == oracle.SOLVED
+        u = _independent_gap_solve(oracle, prm, w["x0"][b].astype(float), w["u_lin"][b].astype(float),
+                                   w["x_ref"][b].astype(float), hs)
+        np.testing.assert_allclose(r["u"], u, atol=1e-6)
+        y = r["y"][3 * (N + 1):3 * (N + 1) + 2 * (N + 1)]
+        active += int((np.abs(y) > 1e-9).any())
+    assert active >= B // 4  # the sample exercises active gap rows
+
+
 @pytest.mark.parametrize("gap", [False, True])
 def test_kkt_certificate(oracle, gap):
     N = 20
@@ -159,6 +212,58 @@ def test_kkt_certificate(oracle, gap):
         Am, Bm, Cm = oracle.linearize(*w["x0"][b][2:3], *w["u_lin"][b])
         for i in range(N):
             np.testing.assert_allclose(r["x"][i + 1], Am @ r["x"][i] + Bm @ r["u"][i] + Cm, atol=1e-12)
+
+
+def test_gi_active_set_full_rank(oracle):
+    """Gap rows + u_des on the speed bound: the GI active set reaches n = 2N rows (QPs 92, 99,
+    160, 214 of this batch). A further row is then dependent by construction; the oracle once
+    added it on a rounding-level pivot and overran its n-slot state (heap corruption)."""
+    rng = np.random.default_rng(7000)
+    N = int(rng.choice([1, 2, 5, 13, 20, 27, 33, 40, 48]))
+    lo0, lo1 = float(rng.uniform(1.0, 3.5)), float(rng.uniform(-0.6, -0.1))
+    hi0, hi1 = lo0 + float(rng.uniform(0.3, 2.0)), -lo1 * float(rng.uniform(0.5, 1.5))
+    ud = [float(rng.choice([hi0, lo0, 0.5 * (lo0 + hi0)])), float(rng.choice([0.0, hi1, lo1]))]
+    q01 = float(rng.choice([0.0, 1.0, 10.0, 40.0]))
+    over = dict(q=[q01, q01 if rng.random() < 0.5 else float(rng.uniform(0.5, 20.0)), float(rng.choice([0.0, 0.5, 3.0]))],
+                r=[float(rng.uniform(0.05, 2.0)), float(rng.uniform(0.5, 10.0))], u_des=ud, u_min=[lo0, lo1],
+                u_max=[hi0, hi1])
+    dt = float(np.float32(rng.choice([0.005, 0.01, 0.02, 0.05])))
+    assert N == 33 and rng.random() < 0.4  # the gap draw of this seed
+    B = 256
+    w = workload.make_batch(B, N, seed=int(rng.integers(1 << 30)), heading="true",
+                            lateral=float(rng.uniform(0.0, 1.5)), steer_range=float(rng.uniform(0.0, 0.8)))
+    ranges, amin, ainc, amax = workload.make_scans(B, seed=int(rng.integers(1 << 30)))
+    prm = oracle.params(N, dt=dt, **over)
+    full = 0
+    for b in (92, 99, 160, 214, 0):
+        rc, l1, l2, _, _ = oracle.find_half_spaces(w["x0"][b].astype(np.float64), ranges[b], amin, ainc, amax)
+        h = np.array([l1, l2], np.float32).astype(np.float64)
+        args = (prm, w["x0"][b].astype(np.float64), w["u_lin"][b].astype(np.float64), w["x_ref"][b].astype(np.float64), h)
+        r = oracle.solve(*args, True)
+        assert r["n_active"] <= 2 * N
+        full += r["n_active"] == 2 * N
+        # feasibility of the assembled QP by an independent LP (HiGHS)
+        feasible = _lp_feasible(oracle.assemble(*args, True))
+        if feasible:
+            assert r["status"] == oracle.SOLVED
+            assert oracle.kkt_residuals(*args[:4], r["z"], r["y"], h, True).max() < 1e-8
+        else:
+            # infeasible; 214 ends GI on a point outside the box: reported uncertified, not SOLVED
+            assert r["status"] in (oracle.PRIMAL_INFEASIBLE, oracle.UNCERTIFIED), (b, r["status"])
+    assert full >= 3
+
+
+def _lp_feasible(A):
+    import scipy.sparse as sp
+    from scipy.optimize import linprog
+
+    n, m = len(A["q"]), len(A["l"])
+    Am = sp.csc_matrix((A["A_val"], A["A_rowind"], A["A_colptr"]), shape=(m, n)).toarray()
+    fl, fu = A["l"] > -1e29, A["u"] < 1e29
+    res = linprog(np.zeros(n), A_ub=np.vstack([Am[fu], -Am[fl]]), b_ub=np.concatenate([A["u"][fu], -A["l"][fl]]),
+                  bounds=(None, None), method="highs")
+    assert res.status in (0, 2), res.message
+    return res.status == 0
 
 
 def infeasible_cases():
