@@ -102,6 +102,7 @@ struct f110qp_ctx {
   int lane_qpw = 0;          // lane QPs per wave (LaneWork::qpw, 0 = auto)
   int lane_rot = 1;          // lane heading-frame kernel when q0 == q1 (LaneWork::rot)
   int lane_dref = 1;         // lane fp64 references in LDS when they fit (LaneWork::dref)
+  int lane_seg = 0;          // lane horizon segments per QP (LaneWork::seg: 0 auto, 1 off, 2/4/8)
   hipStream_t stream = nullptr;
 };
 
@@ -189,6 +190,12 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
   if (const char* er = std::getenv("F110QP_LANE_ROT")) c->lane_rot = std::atoi(er) != 0;
   // test hook: F110QP_LANE_DREF=0 keeps the lane back end's references as floats in LDS
   if (const char* ed = std::getenv("F110QP_LANE_DREF")) c->lane_dref = std::atoi(ed) != 0;
+  // test/bench hook: F110QP_LANE_SEG = horizon segments per QP of the lane back end (0 auto,
+  // 1 off: lane_kernel.h only, 2 / 4 / 8 forced where the horizon and the LDS allow)
+  if (const char* es = std::getenv("F110QP_LANE_SEG")) {
+    const int v = std::atoi(es);
+    if (v == 0 || v == 1 || v == 2 || v == 4 || v == 8) c->lane_seg = v;
+  }
   // test hook: F110QP_PDAS_MAX caps the wave kernel's box PDAS passes (0 = GI from scratch)
   k.pdas_max = 10;
   if (const char* ep = std::getenv("F110QP_PDAS_MAX")) {
@@ -274,6 +281,7 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   lw->qpw = c->lane_qpw;
   lw->rot = c->lane_rot;
   lw->dref = c->lane_dref;
+  lw->seg = c->lane_seg;
   return F110QP_OK;
 }
 
@@ -413,10 +421,26 @@ int f110qp_backend_info(f110qp_ctx* c, int batch, int grouped, int* backend, int
   f110qp::LaneWork lw;
   lw.mode = c->lane_mode;
   lw.qpw = c->lane_qpw;
+  lw.seg = c->lane_seg;
   const bool lane = be == F110QP_BACKEND_LANE;
+  const int segs = lane ? f110qp::lane_segments(c->kp, batch, lw) : 1;
   if (backend) *backend = be;
-  if (qps_per_wave) *qps_per_wave = lane ? f110qp::lane_qps_per_wave(batch, lw.qpw) : 1;
-  if (scratch) *scratch = lane ? f110qp::lane_scratch_mode(c->kp, batch, lw) : 0;
+  if (qps_per_wave) *qps_per_wave = lane ? (segs > 1 ? 64 / segs : f110qp::lane_qps_per_wave(batch, lw.qpw)) : 1;
+  if (scratch) *scratch = lane ? (segs > 1 ? 1 : f110qp::lane_scratch_mode(c->kp, batch, lw)) : 0;
+  return F110QP_OK;
+}
+
+int f110qp_lane_segments(f110qp_ctx* c, int batch, int* segments) {
+  if (!c || !segments) return fail(F110QP_ERR_INVALID, "ctx / segments is NULL");
+  if (batch < 1) return fail(F110QP_ERR_INVALID, "batch must be >= 1");
+  int be = 0;
+  const int rc = f110qp_backend_info(c, batch, 0, &be, nullptr, nullptr);
+  if (rc) return rc;
+  f110qp::LaneWork lw;
+  lw.mode = c->lane_mode;
+  lw.qpw = c->lane_qpw;
+  lw.seg = c->lane_seg;
+  *segments = be == F110QP_BACKEND_LANE ? f110qp::lane_segments(c->kp, batch, lw) : 1;
   return F110QP_OK;
 }
 

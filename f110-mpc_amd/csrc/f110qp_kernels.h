@@ -54,6 +54,7 @@ struct LaneWork {
   int qpw = 0;    // QPs per wave: 0 auto (lane_qps_per_wave), else a power of two <= 64
   int rot = 1;    // 1: heading-frame kernel when q0 == q1 (lane_kernel.h ROT); 0: general frame
   int dref = 1;   // 1: fp64 references in LDS when the resident waves fit (DREF); 0: float
+  int seg = 0;    // horizon segments per QP (lane_seg_kernel.h): 0 auto, 1 off, 2 / 4 / 8 forced
 };
 
 // Optional per-QP objective outputs (fp64, computed in the kernels' output sweeps from the fp64
@@ -70,6 +71,9 @@ constexpr int kLaneTargetWaves = 256;
 int lane_qps_per_wave(int B, int qpw);
 // scratch placement the lane launch picks for a batch: 1 LDS fp64, 2 LDS fp32, 3 HBM fp64, 4 HBM fp32
 int lane_scratch_mode(const KParams& P, int B, const LaneWork& lw);
+// horizon segments per QP the lane launch picks for a batch (1 = lane_kernel.h, one QP per lane
+// group of 64 / L identical lanes; S > 1 = lane_seg_kernel.h, 64 / S QPs per wave)
+int lane_segments(const KParams& P, int B, const LaneWork& lw);
 
 enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
 

@@ -11,6 +11,43 @@
 
 namespace f110qp {
 
+template <int S, bool ROT>
+hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
+                             float* uo, float* xo, int* st, int* its, const WarmState& ws,
+                             const LaneWork& lw, const ObjOut& oo, hipStream_t s);  // lane_seg_inst.hip
+constexpr size_t seg_lds_per_wave(int N, int S) { return (size_t)(N / S) * 64 * (3 * 8 + 4 + 11 * 8); }
+
+// Horizon segments per QP (lane_seg_kernel.h). A batch whose waves leave SIMDs idle (the QPs fit
+// in fewer than one wave per SIMD at 64 / S QPs per wave) splits every QP's horizon over S lanes
+// instead of running 64 / L identical copies of it. S divides N into segments of >= 2 stages, the
+// grid stays within one wave per SIMD (1,024 waves) and the segmented LDS fits. Among those the
+// launch takes the S with the shortest per-pass chain by the instruction model of DESIGN.md 2b:
+// sequential N x ~255 instructions, segmented (N / S) x ~350 + (S - 1) x ~230 (the two segment
+// recursions). A forced QPs-per-wave or scratch placement keeps lane_kernel.h.
+int lane_segments(const KParams& P, int B, const LaneWork& lw) {
+  const int N = P.N;
+  auto fits = [&](int S) {
+    if (N % S != 0 || N / S < 2) return false;
+    const size_t waves = ((size_t)B * S + 63) / 64;
+    const size_t per_cu = (waves + 255) / 256;
+    return per_cu <= 4 && per_cu * seg_lds_per_wave(N, S) <= 160 * 1024;
+  };
+  if (lw.seg == 1) return 1;
+  if (lw.seg == 2 || lw.seg == 4 || lw.seg == 8) return fits(lw.seg) ? lw.seg : 1;
+  if (lw.qpw != 0 || (lw.mode != 0 && lw.mode != 1)) return 1;
+  int best = 1;
+  double cbest = 255.0 * N;
+  for (int S = 2; S <= 8; S <<= 1) {
+    if (!fits(S)) continue;
+    const double c = 350.0 * (N / S) + 230.0 * (S - 1);
+    if (c < cbest) {
+      best = S;
+      cbest = c;
+    }
+  }
+  return best;
+}
+
 #ifndef F110QP_LANE_ALL
 template <typename ST, bool SLDS, int L, bool ROT, bool DREF>
 hipError_t launch_lane_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
@@ -99,6 +136,16 @@ hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* ul
                        const float* xr, float* uo, float* xo, int* st, int* its,
                        const WarmState& ws, const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
+  const bool rot = lw.rot && P.q[0] == P.q[1];
+  switch (lane_segments(P, B, lw)) {
+    case 2: return rot ? launch_lane_seg_t<2, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s)
+                       : launch_lane_seg_t<2, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    case 4: return rot ? launch_lane_seg_t<4, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s)
+                       : launch_lane_seg_t<4, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    case 8: return rot ? launch_lane_seg_t<8, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s)
+                       : launch_lane_seg_t<8, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    default: break;
+  }
   switch (lane_qps_per_wave(B, lw.qpw)) {
     case 1: return launch_lq<1>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
     case 2: return launch_lq<2>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);

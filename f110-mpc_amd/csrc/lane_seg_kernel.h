@@ -1,0 +1,634 @@
+// lane_seg_kernel.h — the lane back end for batches that leave lanes over: ONE QP PER S LANES,
+// each lane owning one of S horizon segments (a partitioned, parallel-in-time Riccati).
+//
+// lane_kernel.h solves L <= 64 QPs per wave and, below 64 QPs per wave, runs 64 / L identical
+// copies of each QP to keep EXEC full: a QP's time is its serial chain of N backward Riccati
+// stages + N forward stages per PDAS pass (mpc.cpp:244-248 block-tridiagonal KKT walked
+// strictly in sequence). Here the S = 64 / L lanes of a QP split the horizon into segments
+// [s_j, e_j) of m = N / S stages and every pass runs:
+//
+// 1. backward, all segments at once: the masked Riccati step of lane_kernel.h over the lane's m
+//    stages, with the terminal value V_e(x_e) = lam_j' x_e (lam_j: the multiplier of the coupling
+//    x_e^(j) = x_s^(j+1), unknown yet; the last segment keeps the true terminal cost, mpc.cpp:228),
+//    and alongside it the affine map of the segment's closed loop x_e = Phi x_s + psi + Gam lam_j:
+//      W = Phi_{i+1} B,  F_i = -S_i^-1 W'  (the lam-gain of u_i, S_i^-1 the masked inverse),
+//      psi_i = W k_i + Phi_{i+1} C + psi_{i+1},  Gam_i = Gam_{i+1} + W F_i,
+//      Phi_i = Phi_{i+1} A + W K_i             (Phi_e = I, psi_e = 0, Gam_e = 0).
+//    At the segment start V_s(x) = 1/2 x'P_s x + (a_s + Phi' lam_j)' x + const.
+// 2. the segment ends: the coupling conditions x_s^(j+1) = Phi_j x_s^(j) + psi_j + Gam_j lam_j and
+//    lam_{j-1} = P_j x_s^(j) + a_j + Phi_j' lam_j (x_s^(0) = 0) are an S-stage LQ two-point
+//    boundary problem, solved by a Riccati recursion over the segments, lam_{j-1} = M_j x + m_j:
+//      T_j = (I - M_{j+1} Gam_j)^-1 M_{j+1} Phi_j,  t_j = (I - M_{j+1} Gam_j)^-1 (M_{j+1} psi_j + m_{j+1}),
+//      M_j = P_j + Phi_j' T_j,  m_j = a_j + Phi_j' t_j,   then lam_j = T_j x_s^(j) + t_j forward.
+//    (I - M Gam has eigenvalues >= 1: M is positive definite, Gam negative semidefinite.) Every
+//    lane runs every step on its own data with its neighbour's (M, m) / x_e from a lane shuffle;
+//    the top segment's (Phi, psi, Gam) are zeroed so that its lane reproduces (P, a) and hands
+//    x_e = 0 to segment 0 round the ring: S - 1 identical steps each way, no selects.
+// 3. refresh, all segments: the lam-part of the feed-forward, p^lam_e = lam_j,
+//    k_i += -S_i^-1 B' p^lam_{i+1},  p^lam_i = A' p^lam_{i+1} + K_i' B' p^lam_{i+1}
+//    (the p-recursion of the Riccati step restricted to its lam-dependent part).
+// 4. forward, all segments: lane_kernel.h's sweep from x_s^(j) with the costate
+//    P_s x_s + a_s + p^lam_s: rollout, costate carried forward, PDAS re-guess per stage.
+// A pass's result equals the sequential pass's up to rounding (tests/diag_segment_riccati_model.py:
+// 1.8e-15 relative on random masks), so the PDAS iterates, the single-flip rule (the first
+// violation over the whole horizon: a min over the QP's lanes) and the stopping test are
+// lane_kernel.h's. Per pass the chain is m stages of ~(200 + 120 + 30) instructions plus
+// 2 (S - 1) segment steps instead of N stages of ~255.
+//
+// Layout (fp64 throughout): lane l = slot + L j works on QP L w + slot, segment j. LDS per wave,
+// lane-major so that every access is one conflict-free 64-lane row: references [3m][64] (recentred,
+// rotated), PDAS state [m][64] int, Riccati scratch [m][11][64] (K 6, k 2, S^-1 3); the float
+// staging of the references borrows the scratch region.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "f110qp_kernels.h"
+
+namespace f110qp {
+
+// LDS bytes per wave of the segmented kernel for horizon N split into S segments
+constexpr size_t seg_lds_bytes(int N, int S) { return (size_t)(N / S) * 64 * (3 * 8 + 4 + 11 * 8); }
+
+template <int S>
+__device__ __forceinline__ double seg_shfl(double v, int src) {
+  return __shfl(v, src, 64);
+}
+
+template <int S, bool ROT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void lane_seg_kernel(
+    const KParams P, const int B, const float* __restrict__ x0g, const float* __restrict__ ulg,
+    const float* __restrict__ xrg, float* __restrict__ uout, float* __restrict__ xout,
+    int* __restrict__ status_out, int* __restrict__ iters_out, const WarmState ws, const int kmax,
+    const ObjOut oo) {
+  constexpr int L = 64 / S;  // QPs per wave
+  extern __shared__ __attribute__((aligned(16))) double seg_smem[];
+  const int lane = threadIdx.x;
+  const int sl = lane & (L - 1);
+  const int seg = lane / L;
+  const int b0 = blockIdx.x * L;
+  const int nq = (B - b0) < L ? (B - b0) : L;
+  const int slot = sl < nq ? sl : 0;  // a missing QP's lanes duplicate QP 0 of the wave
+  const bool owner = sl < nq;          // stores the outputs of its segment's stages
+  const bool qowner = owner && seg == 0;
+  const int b = b0 + slot;
+  const int N = P.N;
+  const int m = N / S;
+  const int s0 = seg * m;
+  const bool top = seg == S - 1;
+  const int up = (lane + L) & 63, dn = (lane - L) & 63;  // same QP, segment + 1 / - 1 (ring)
+
+  double* const r64 = seg_smem + lane;                                   // [3m][64]
+  int* const ap = reinterpret_cast<int*>(seg_smem + 3 * m * 64) + lane;  // [m][64]
+  double* const sc = seg_smem + 3 * m * 64 + m * 32 + lane;              // [m][11][64]
+
+  // ---- stage the wave's reference paths (float, [3N][L]) into the scratch region ----
+  unsigned long long badq = 0ull;
+  {
+    float* stg = reinterpret_cast<float*>(seg_smem + 3 * m * 64 + m * 32);
+    const int n3 = 3 * N;
+    const int S3 = 3 * P.xr_stride;
+    const int tot = nq * n3;
+    const float* src = xrg + (size_t)b0 * S3;
+    const float rn3 = 1.0f / (float)n3;
+    constexpr int kChunk = 8;
+    for (int e0 = 0; e0 < tot; e0 += kChunk * 64) {
+      float vbuf[kChunk];
+      int dst[kChunk];
+#pragma unroll
+      for (int j = 0; j < kChunk; j++) {
+        const int e = e0 + j * 64 + lane;
+        int q = (int)((float)e * rn3);
+        q -= (q * n3 > e) ? 1 : 0;
+        q += ((q + 1) * n3 <= e) ? 1 : 0;
+        const int c = e - q * n3;
+        dst[j] = (e < tot) ? c * L + q : -1;
+        vbuf[j] = (e < tot) ? src[(size_t)q * S3 + c] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < kChunk; j++) {
+        if (dst[j] >= 0) stg[dst[j]] = vbuf[j];
+        if (!isfinite(vbuf[j])) badq |= 1ull << (dst[j] & (L - 1));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const unsigned lo = __shfl_xor((unsigned)badq, o), hi = __shfl_xor((unsigned)(badq >> 32), o);
+      badq |= ((unsigned long long)hi << 32) | lo;
+    }
+    __syncthreads();
+  }
+
+  // ---- per-lane QP data (Model::Linearize, model.cpp:30-59), as lane_kernel.h ----
+  const double X0 = (double)x0g[3 * b + 0], Y0 = (double)x0g[3 * b + 1];
+  const float fTH0 = x0g[3 * b + 2];
+  const double th0 = (double)fTH0;
+  const double v = (double)ulg[2 * b + 0], d = (double)ulg[2 * b + 1];
+  const double dt = (double)P.dt;
+  const double Lw = (double)0.3302f;
+  double sn, cs, sd, cd;
+  sincos(th0, &sn, &cs);
+  sincos(d, &sd, &cd);
+  const double sec2 = 1.0 / (cd * cd);
+  const double a02 = ROT ? 0.0 : -1 * v * sn * dt;                    // model.cpp:42
+  const double a12 = ROT ? v * dt : v * cs * dt;                      // :43
+  const double b00 = ROT ? dt : cs * dt, b10 = ROT ? 0.0 : sn * dt;   // :48-49
+  const double b20 = (sd / cd) * dt / Lw, b21 = v * sec2 * dt / Lw;   // :50-51
+  const double c0r = v * th0 * sn * dt, c1r = -1 * v * th0 * cs * dt;  // :53-54
+  const double c2 = -1 * d * v * sec2 * dt / Lw;                      // :55
+  const double c0 = ROT ? 0.0 : c0r + a02 * th0, c1 = ROT ? 0.0 : c1r + a12 * th0;
+  const double q0 = P.q[0], q1 = P.q[1], q2 = P.q[2], r0 = P.r[0], r1 = P.r[1];
+  const double ud0 = P.udes[0], ud1 = P.udes[1];
+  const double lb0 = (double)P.umin[0], lb1 = (double)P.umin[1];
+  const double ub0 = (double)P.umax[0], ub1 = (double)P.umax[1];
+  // PDAS flip tolerances of lane_kernel.h's fp64-scratch kernels (1e-10, scaled)
+  const double pt = 1e-10, gt = 1e-10;
+  const double lbe0 = lb0 - pt * (1.0 + fabs(lb0)), ube0 = ub0 + pt * (1.0 + fabs(ub0));
+  const double lbe1 = lb1 - pt * (1.0 + fabs(lb1)), ube1 = ub1 + pt * (1.0 + fabs(ub1));
+  const double gtol0 = gt * (1.0 + r0 * (1.0 + fabs(lb0) + fabs(ub0)));
+  const double gtol1 = gt * (1.0 + r1 * (1.0 + fabs(lb1) + fabs(ub1)));
+
+  // references of the lane's stages: recentred (ROT: rotated) fp64, lane-major
+  {
+    const float* stg = reinterpret_cast<const float*>(seg_smem + 3 * m * 64 + m * 32);
+    for (int t = 0; t < m; t++) {
+      const int i = s0 + t;
+      const double dx = (double)stg[(3 * i + 0) * L + slot] - X0;
+      const double dy = (double)stg[(3 * i + 1) * L + slot] - Y0;
+      r64[(3 * t + 0) * 64] = ROT ? cs * dx + sn * dy : dx;
+      r64[(3 * t + 1) * 64] = ROT ? cs * dy - sn * dx : dy;
+      r64[(3 * t + 2) * 64] = (double)stg[(3 * i + 2) * L + slot] - th0;
+    }
+    __syncthreads();  // the staging region becomes the Riccati scratch
+  }
+  // terminal reference x_ref[N-1] (mpc.cpp:228): the last stage of the top segment
+  const double rNx = __shfl(r64[(3 * (m - 1) + 0) * 64], (lane | (63 & ~(L - 1))) & 63);
+  const double rNy = __shfl(r64[(3 * (m - 1) + 1) * 64], (lane | (63 & ~(L - 1))) & 63);
+  const double rNt = __shfl(r64[(3 * (m - 1) + 2) * 64], (lane | (63 & ~(L - 1))) & 63);
+
+  // warm start: previous tick's active bounds when the slot's (theta0, v, steer) bits repeat
+  const int R = (2 * N + 63) / 64;
+  const unsigned kth = __float_as_uint(fTH0), kv = __float_as_uint(ulg[2 * b + 0]);
+  const unsigned kd = __float_as_uint(ulg[2 * b + 1]);
+  {
+    unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
+    bool hit = false;
+    if (ws.act && ws.key) {
+      const unsigned* key = ws.key + 4 * b;
+      hit = key[3] != 0u && key[0] == kth && key[1] == kv && key[2] == kd;
+    }
+    if (hit) {
+      lo0 = ws.act[2 * R * b];
+      hi0 = ws.act[2 * R * b + 1];
+      if (R > 1) {
+        lo1 = ws.act[2 * (R * b + 1)];
+        hi1 = ws.act[2 * (R * b + 1) + 1];
+      }
+    }
+    for (int t = 0; t < m; t++) {
+      const int i = s0 + t;
+      int st = 0;
+#pragma unroll
+      for (int a = 0; a < 2; a++) {
+        const int va = 2 * i + a;
+        const unsigned long long l = va < 64 ? lo0 : lo1, h = va < 64 ? hi0 : hi1;
+        const int ca = ((l >> (va & 63)) & 1ull) ? 1 : (((h >> (va & 63)) & 1ull) ? 2 : 0);
+        st |= ca << (2 * a);
+      }
+      ap[t * 64] = st;
+    }
+  }
+
+  const bool bad = !(isfinite(X0) && isfinite(Y0) && isfinite(th0) && isfinite(v) && isfinite(d)) ||
+                   ((badq >> slot) & 1ull);
+  bool done = bad;
+  int iters = 0;
+  // the segment's start state of the current pass (kept for the output sweep)
+  double xs0 = 0.0, xs1 = 0.0, xs2 = 0.0;
+
+  // wave-uniform fold of a ballot over the QP's S lanes: bit sl set if any segment's bit is
+  auto fold = [&](unsigned long long mk) {
+#pragma unroll
+    for (int k = L; k < 64; k <<= 1) mk |= mk >> k;
+    return mk;
+  };
+
+  const int max_pass = P.max_iter > kmax ? P.max_iter : kmax;
+  for (int pass = 0; pass < max_pass; pass++) {
+    if (__ballot(!done) == 0ull) break;
+    const bool single = pass >= kmax;
+    // ---- 1. backward over the segment: Riccati + the closed-loop map (Phi, psi, Gam) ----
+    double P00 = top ? q0 : 0.0, P01 = 0.0, P02 = 0.0, P11 = top ? q1 : 0.0, P12 = 0.0;
+    double P22 = top ? q2 : 0.0;
+    double p0 = top ? -q0 * rNx : 0.0, p1 = top ? -q1 * rNy : 0.0, p2 = top ? -q2 * rNt : 0.0;
+    double F00 = 1.0, F01 = 0.0, F02 = 0.0, F10 = 0.0, F11 = 1.0, F12 = 0.0, F20 = 0.0, F21 = 0.0;
+    double F22 = 1.0;  // Phi
+    double s0v = 0.0, s1v = 0.0, s2v = 0.0;  // psi
+    double G00 = 0.0, G01 = 0.0, G02 = 0.0, G11 = 0.0, G12 = 0.0, G22 = 0.0;  // Gam (symmetric)
+    {
+      int nst = ap[(m - 1) * 64];
+      double rx = r64[(3 * (m - 1) + 0) * 64], ry = r64[(3 * (m - 1) + 1) * 64];
+      double rt = r64[(3 * (m - 1) + 2) * 64];
+      for (int t = m - 1; t >= 0; t--) {
+        double* s = sc + t * 11 * 64;
+        const int sti = nst;
+        const int tn = t > 0 ? t - 1 : 0;
+        nst = ap[tn * 64];
+        const double rxi = rx, ryi = ry, rti = rt;
+        rx = r64[(3 * tn + 0) * 64];
+        ry = r64[(3 * tn + 1) * 64];
+        rt = r64[(3 * tn + 2) * 64];
+        const double g0 = ROT ? P02 * c2 + p0 : P00 * c0 + P01 * c1 + P02 * c2 + p0;
+        const double g1 = ROT ? P12 * c2 + p1 : P01 * c0 + P11 * c1 + P12 * c2 + p1;
+        const double g2 = ROT ? P22 * c2 + p2 : P02 * c0 + P12 * c1 + P22 * c2 + p2;
+        const double pb0 = ROT ? P00 * b00 + P02 * b20 : P00 * b00 + P01 * b10 + P02 * b20;
+        const double pb1 = ROT ? P01 * b00 + P12 * b20 : P01 * b00 + P11 * b10 + P12 * b20;
+        const double pb2 = ROT ? P02 * b00 + P22 * b20 : P02 * b00 + P12 * b10 + P22 * b20;
+        const double pc0 = P02 * b21, pc1 = P12 * b21, pc2 = P22 * b21;
+        const double H00 = ROT ? r0 + b00 * pb0 + b20 * pb2 : r0 + b00 * pb0 + b10 * pb1 + b20 * pb2;
+        const double H01 = b21 * pb2;
+        const double H11 = r1 + b21 * pc2;
+        const double X00 = pb0, X01 = pb1;
+        const double X02 = ROT ? pb2 + a12 * pb1 : pb2 + a02 * pb0 + a12 * pb1;
+        const double X10 = pc0, X11 = pc1;
+        const double X12 = ROT ? pc2 + a12 * pc1 : pc2 + a02 * pc0 + a12 * pc1;
+        const double h0 = ROT ? -r0 * ud0 + b00 * g0 + b20 * g2
+                              : -r0 * ud0 + b00 * g0 + b10 * g1 + b20 * g2;
+        const double h1 = -r1 * ud1 + b21 * g2;
+        const double e0 = ROT ? P02 + a12 * P01 : P02 + a02 * P00 + a12 * P01;
+        const double e1 = ROT ? P12 + a12 * P11 : P12 + a02 * P01 + a12 * P11;
+        const double e2 = ROT ? P22 + a12 * P12 : P22 + a02 * P02 + a12 * P12;
+        const double Y00 = q0 + P00, Y01 = P01, Y11 = q1 + P11, Y02 = e0, Y12 = e1;
+        const double Y22 = ROT ? q2 + e2 + a12 * e1 : q2 + e2 + a02 * e0 + a12 * e1;
+        const double hx0 = -q0 * rxi + g0, hx1 = -q1 * ryi + g1;
+        const double hx2 = ROT ? -q2 * rti + g2 + a12 * g1 : -q2 * rti + g2 + a02 * g0 + a12 * g1;
+        const int ca0 = sti & 3, ca1 = (sti >> 2) & 3;
+        const bool f0 = ca0 == 0, f1 = ca1 == 0;
+        const double bA0 = f0 ? 0.0 : (ca0 == 1 ? lb0 : ub0);
+        const double bA1 = f1 ? 0.0 : (ca1 == 1 ? lb1 : ub1);
+        const double M00 = f0 ? H00 : 1.0, M11 = f1 ? H11 : 1.0, M01 = (f0 && f1) ? H01 : 0.0;
+        const double det = M00 * M11 - M01 * M01;
+        double idet = __builtin_amdgcn_rcp(det);
+        idet = fma(idet, fma(-det, idet, 1.0), idet);
+        idet = fma(idet, fma(-det, idet, 1.0), idet);
+        const double I00 = f0 ? M11 * idet : 0.0, I11 = f1 ? M00 * idet : 0.0;
+        const double I01 = (f0 && f1) ? -M01 * idet : 0.0;
+        const double K00 = -I00 * X00 - I01 * X10, K01 = -I00 * X01 - I01 * X11;
+        const double K02 = -I00 * X02 - I01 * X12;
+        const double K10 = -I01 * X00 - I11 * X10, K11 = -I01 * X01 - I11 * X11;
+        const double K12 = -I01 * X02 - I11 * X12;
+        const double w0 = h0 + H00 * bA0 + H01 * bA1, w1 = h1 + H01 * bA0 + H11 * bA1;
+        const double k0 = bA0 - (I00 * w0 + I01 * w1), k1 = bA1 - (I01 * w0 + I11 * w1);
+        s[0] = K00; s[64] = K01; s[2 * 64] = K02; s[3 * 64] = K10; s[4 * 64] = K11;
+        s[5 * 64] = K12; s[6 * 64] = k0; s[7 * 64] = k1;
+        s[8 * 64] = I00; s[9 * 64] = I01; s[10 * 64] = I11;
+        P00 = Y00 + X00 * K00 + X10 * K10;
+        P01 = Y01 + X00 * K01 + X10 * K11;
+        P02 = Y02 + X00 * K02 + X10 * K12;
+        P11 = Y11 + X01 * K01 + X11 * K11;
+        P12 = Y12 + X01 * K02 + X11 * K12;
+        P22 = Y22 + X02 * K02 + X12 * K12;
+        p0 = hx0 + X00 * k0 + X10 * k1;
+        p1 = hx1 + X01 * k0 + X11 * k1;
+        p2 = hx2 + X02 * k0 + X12 * k1;
+        // closed-loop map of the segment (Phi = Phi_{i+1} on entry)
+        const double W00 = ROT ? F00 * b00 + F02 * b20 : F00 * b00 + F01 * b10 + F02 * b20;  // Phi B
+        const double W10 = ROT ? F10 * b00 + F12 * b20 : F10 * b00 + F11 * b10 + F12 * b20;
+        const double W20 = ROT ? F20 * b00 + F22 * b20 : F20 * b00 + F21 * b10 + F22 * b20;
+        const double W01 = F02 * b21, W11 = F12 * b21, W21 = F22 * b21;
+        // lam-gain of u_i: Fl = -S^-1 W'
+        const double L00 = -(I00 * W00 + I01 * W01), L01 = -(I00 * W10 + I01 * W11);
+        const double L02 = -(I00 * W20 + I01 * W21);
+        const double L10 = -(I01 * W00 + I11 * W01), L11 = -(I01 * W10 + I11 * W11);
+        const double L12 = -(I01 * W20 + I11 * W21);
+        // psi += W k + Phi C
+        s0v += W00 * k0 + W01 * k1 + (ROT ? F02 * c2 : F00 * c0 + F01 * c1 + F02 * c2);
+        s1v += W10 * k0 + W11 * k1 + (ROT ? F12 * c2 : F10 * c0 + F11 * c1 + F12 * c2);
+        s2v += W20 * k0 + W21 * k1 + (ROT ? F22 * c2 : F20 * c0 + F21 * c1 + F22 * c2);
+        // Gam += W Fl
+        G00 += W00 * L00 + W01 * L10;
+        G01 += W00 * L01 + W01 * L11;
+        G02 += W00 * L02 + W01 * L12;
+        G11 += W10 * L01 + W11 * L11;
+        G12 += W10 * L02 + W11 * L12;
+        G22 += W20 * L02 + W21 * L12;
+        // Phi = Phi A + W K  (A = I + E, E = a02 e_0 e_2' + a12 e_1 e_2')
+        const double n02 = (ROT ? F02 + a12 * F01 : F02 + a02 * F00 + a12 * F01) + W00 * K02 + W01 * K12;
+        const double n12 = (ROT ? F12 + a12 * F11 : F12 + a02 * F10 + a12 * F11) + W10 * K02 + W11 * K12;
+        const double n22 = (ROT ? F22 + a12 * F21 : F22 + a02 * F20 + a12 * F21) + W20 * K02 + W21 * K12;
+        F00 += W00 * K00 + W01 * K10; F01 += W00 * K01 + W01 * K11;
+        F10 += W10 * K00 + W11 * K10; F11 += W10 * K01 + W11 * K11;
+        F20 += W20 * K00 + W21 * K10; F21 += W20 * K01 + W21 * K11;
+        F02 = n02; F12 = n12; F22 = n22;
+      }
+    }
+    // ---- 2. the segment ends: Riccati over the segments, then lam_j, x_s^(j) forward ----
+    // the top segment hands (P, a) up the chain and x_e = 0 round the ring to segment 0
+    if (top) {
+      F00 = F01 = F02 = F10 = F11 = F12 = F20 = F21 = F22 = 0.0;
+      s0v = s1v = s2v = 0.0;
+      G00 = G01 = G02 = G11 = G12 = G22 = 0.0;
+    }
+    double lm0 = 0.0, lm1 = 0.0, lm2 = 0.0;  // lam_j
+    xs0 = xs1 = xs2 = 0.0;
+    if constexpr (S > 1) {
+      double M00 = P00, M01 = P01, M02 = P02, M11 = P11, M12 = P12, M22 = P22;
+      double m0 = p0, m1 = p1, m2 = p2;
+      double T00 = 0, T01 = 0, T02 = 0, T10 = 0, T11 = 0, T12 = 0, T20 = 0, T21 = 0, T22 = 0;
+      double t0 = 0, t1 = 0, t2 = 0;
+#pragma unroll 1
+      for (int it = 0; it < S - 1; it++) {
+        const double N00 = seg_shfl<S>(M00, up), N01 = seg_shfl<S>(M01, up), N02 = seg_shfl<S>(M02, up);
+        const double N11 = seg_shfl<S>(M11, up), N12 = seg_shfl<S>(M12, up), N22 = seg_shfl<S>(M22, up);
+        const double n0 = seg_shfl<S>(m0, up), n1 = seg_shfl<S>(m1, up), n2 = seg_shfl<S>(m2, up);
+        // Z = I - Mn Gam
+        const double Z00 = 1.0 - (N00 * G00 + N01 * G01 + N02 * G02);
+        const double Z01 = -(N00 * G01 + N01 * G11 + N02 * G12);
+        const double Z02 = -(N00 * G02 + N01 * G12 + N02 * G22);
+        const double Z10 = -(N01 * G00 + N11 * G01 + N12 * G02);
+        const double Z11 = 1.0 - (N01 * G01 + N11 * G11 + N12 * G12);
+        const double Z12 = -(N01 * G02 + N11 * G12 + N12 * G22);
+        const double Z20 = -(N02 * G00 + N12 * G01 + N22 * G02);
+        const double Z21 = -(N02 * G01 + N12 * G11 + N22 * G12);
+        const double Z22 = 1.0 - (N02 * G02 + N12 * G12 + N22 * G22);
+        // Z^-1 by the adjugate
+        const double A00 = Z11 * Z22 - Z12 * Z21, A01 = Z02 * Z21 - Z01 * Z22, A02 = Z01 * Z12 - Z02 * Z11;
+        const double A10 = Z12 * Z20 - Z10 * Z22, A11 = Z00 * Z22 - Z02 * Z20, A12 = Z02 * Z10 - Z00 * Z12;
+        const double A20 = Z10 * Z21 - Z11 * Z20, A21 = Z01 * Z20 - Z00 * Z21, A22 = Z00 * Z11 - Z01 * Z10;
+        const double zdet = Z00 * A00 + Z01 * A10 + Z02 * A20;
+        double iz = __builtin_amdgcn_rcp(zdet);
+        iz = fma(iz, fma(-zdet, iz, 1.0), iz);
+        iz = fma(iz, fma(-zdet, iz, 1.0), iz);
+        // Mn Phi and Mn psi + mn
+        const double U00 = N00 * F00 + N01 * F10 + N02 * F20, U01 = N00 * F01 + N01 * F11 + N02 * F21;
+        const double U02 = N00 * F02 + N01 * F12 + N02 * F22;
+        const double U10 = N01 * F00 + N11 * F10 + N12 * F20, U11 = N01 * F01 + N11 * F11 + N12 * F21;
+        const double U12 = N01 * F02 + N11 * F12 + N12 * F22;
+        const double U20 = N02 * F00 + N12 * F10 + N22 * F20, U21 = N02 * F01 + N12 * F11 + N22 * F21;
+        const double U22 = N02 * F02 + N12 * F12 + N22 * F22;
+        const double u0 = N00 * s0v + N01 * s1v + N02 * s2v + n0;
+        const double u1 = N01 * s0v + N11 * s1v + N12 * s2v + n1;
+        const double u2 = N02 * s0v + N12 * s1v + N22 * s2v + n2;
+        T00 = iz * (A00 * U00 + A01 * U10 + A02 * U20); T01 = iz * (A00 * U01 + A01 * U11 + A02 * U21);
+        T02 = iz * (A00 * U02 + A01 * U12 + A02 * U22);
+        T10 = iz * (A10 * U00 + A11 * U10 + A12 * U20); T11 = iz * (A10 * U01 + A11 * U11 + A12 * U21);
+        T12 = iz * (A10 * U02 + A11 * U12 + A12 * U22);
+        T20 = iz * (A20 * U00 + A21 * U10 + A22 * U20); T21 = iz * (A20 * U01 + A21 * U11 + A22 * U21);
+        T22 = iz * (A20 * U02 + A21 * U12 + A22 * U22);
+        t0 = iz * (A00 * u0 + A01 * u1 + A02 * u2);
+        t1 = iz * (A10 * u0 + A11 * u1 + A12 * u2);
+        t2 = iz * (A20 * u0 + A21 * u1 + A22 * u2);
+        // M = P + Phi' T, m = a + Phi' t
+        M00 = P00 + F00 * T00 + F10 * T10 + F20 * T20;
+        M01 = P01 + F00 * T01 + F10 * T11 + F20 * T21;
+        M02 = P02 + F00 * T02 + F10 * T12 + F20 * T22;
+        M11 = P11 + F01 * T01 + F11 * T11 + F21 * T21;
+        M12 = P12 + F01 * T02 + F11 * T12 + F21 * T22;
+        M22 = P22 + F02 * T02 + F12 * T12 + F22 * T22;
+        m0 = p0 + F00 * t0 + F10 * t1 + F20 * t2;
+        m1 = p1 + F01 * t0 + F11 * t1 + F21 * t2;
+        m2 = p2 + F02 * t0 + F12 * t1 + F22 * t2;
+      }
+#pragma unroll 1
+      for (int it = 0; it < S - 1; it++) {
+        const double l0 = T00 * xs0 + T01 * xs1 + T02 * xs2 + t0;
+        const double l1 = T10 * xs0 + T11 * xs1 + T12 * xs2 + t1;
+        const double l2 = T20 * xs0 + T21 * xs1 + T22 * xs2 + t2;
+        const double e0 = F00 * xs0 + F01 * xs1 + F02 * xs2 + s0v + G00 * l0 + G01 * l1 + G02 * l2;
+        const double e1 = F10 * xs0 + F11 * xs1 + F12 * xs2 + s1v + G01 * l0 + G11 * l1 + G12 * l2;
+        const double e2 = F20 * xs0 + F21 * xs1 + F22 * xs2 + s2v + G02 * l0 + G12 * l1 + G22 * l2;
+        xs0 = seg_shfl<S>(e0, dn);
+        xs1 = seg_shfl<S>(e1, dn);
+        xs2 = seg_shfl<S>(e2, dn);
+      }
+      lm0 = top ? 0.0 : T00 * xs0 + T01 * xs1 + T02 * xs2 + t0;
+      lm1 = top ? 0.0 : T10 * xs0 + T11 * xs1 + T12 * xs2 + t1;
+      lm2 = top ? 0.0 : T20 * xs0 + T21 * xs1 + T22 * xs2 + t2;
+    }
+    // ---- 3. refresh: the lam-part of the feed-forward, backward over the segment ----
+    double pl0 = lm0, pl1 = lm1, pl2 = lm2;
+    if constexpr (S > 1) {
+      // stage t - 1's values are loaded while stage t computes (clamped: no branch)
+      double nr[11];
+#pragma unroll
+      for (int e = 0; e < 11; e++) nr[e] = sc[((m - 1) * 11 + e) * 64];
+      for (int t = m - 1; t >= 0; t--) {
+        double* s = sc + t * 11 * 64;
+        const double K00 = nr[0], K01 = nr[1], K02 = nr[2], K10 = nr[3], K11 = nr[4];
+        const double K12 = nr[5], k0 = nr[6], k1 = nr[7];
+        const double I00 = nr[8], I01 = nr[9], I11 = nr[10];
+        {
+          const double* sn1 = sc + (t > 0 ? t - 1 : 0) * 11 * 64;
+#pragma unroll
+          for (int e = 0; e < 11; e++) nr[e] = sn1[e * 64];
+        }
+        const double bp0 = ROT ? b00 * pl0 + b20 * pl2 : b00 * pl0 + b10 * pl1 + b20 * pl2;  // B' p
+        const double bp1 = b21 * pl2;
+        s[6 * 64] = k0 - (I00 * bp0 + I01 * bp1);
+        s[7 * 64] = k1 - (I01 * bp0 + I11 * bp1);
+        const double n0 = pl0 + K00 * bp0 + K10 * bp1, n1 = pl1 + K01 * bp0 + K11 * bp1;
+        pl2 = (ROT ? pl2 + a12 * pl1 : pl2 + a02 * pl0 + a12 * pl1) + K02 * bp0 + K12 * bp1;
+        pl0 = n0; pl1 = n1;
+      }
+    }
+    // ---- 4. forward over the segment: rollout, costate, PDAS re-guess ----
+    bool changed = false;
+    int fi = N;      // single-flip passes: this segment's first flip (stage) ...
+    int fold_st = 0;  // ... and the state it replaced
+    {
+      double x0 = xs0, x1 = xs1, x2 = xs2;
+      double l0 = P00 * x0 + P01 * x1 + P02 * x2 + p0 + pl0;  // costate at x_s
+      double l1 = P01 * x0 + P11 * x1 + P12 * x2 + p1 + pl1;
+      double l2 = P02 * x0 + P12 * x1 + P22 * x2 + p2 + pl2;
+      bool flipped = false;
+      double rx = r64[0], ry = r64[64], rt = r64[2 * 64];
+      int old_n = ap[0];
+      double ng[8];  // stage t + 1's gains, loaded while stage t computes
+#pragma unroll
+      for (int e = 0; e < 8; e++) ng[e] = sc[e * 64];
+      for (int t = 0; t < m; t++) {
+        const double K00 = ng[0], K01 = ng[1], K02 = ng[2], K10 = ng[3], K11 = ng[4];
+        const double K12 = ng[5], k0 = ng[6], k1 = ng[7];
+        {
+          const double* sn1 = sc + (t + 1 < m ? t + 1 : m - 1) * 11 * 64;
+#pragma unroll
+          for (int e = 0; e < 8; e++) ng[e] = sn1[e * 64];
+        }
+        const int old = old_n;
+        const double rxi = rx, ryi = ry, rti = rt;
+        {
+          const int tn = t + 1 < m ? t + 1 : m - 1;
+          old_n = ap[tn * 64];
+          rx = r64[(3 * tn + 0) * 64];
+          ry = r64[(3 * tn + 1) * 64];
+          rt = r64[(3 * tn + 2) * 64];
+        }
+        const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
+        const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
+        const double w0 = l0 - q0 * (x0 - rxi), w1 = l1 - q1 * (x1 - ryi);
+        const double w2 = l2 - q2 * (x2 - rti);
+        l0 = w0; l1 = w1; l2 = ROT ? w2 - a12 * w1 : w2 - a02 * w0 - a12 * w1;
+        const double g0 = ROT ? r0 * (u0 - ud0) + b00 * l0 + b20 * l2
+                              : r0 * (u0 - ud0) + b00 * l0 + b10 * l1 + b20 * l2;
+        const double g1 = r1 * (u1 - ud1) + b21 * l2;
+        int st = old;
+#pragma unroll
+        for (int a = 0; a < 2; a++) {
+          const int ca = (old >> (2 * a)) & 3;
+          const double u = a ? u1 : u0, g = a ? g1 : g0;
+          const double gta = a ? gtol1 : gtol0;
+          const bool nlo = ((ca == 1) & (g > -gta)) | ((ca == 0) & (u < (a ? lbe1 : lbe0)));
+          const bool nhi = !nlo & (((ca == 2) & (g < gta)) | ((ca == 0) & (u > (a ? ube1 : ube0))));
+          const int nca = (int)nlo | ((int)nhi << 1);
+          const bool take = (nca != ca) & !(single & flipped);
+          st = take ? ((st & ~(3 << (2 * a))) | (nca << (2 * a))) : st;
+          flipped |= take;
+        }
+        const bool ch = st != old;
+        fi = (ch & (fi == N)) ? s0 + t : fi;
+        fold_st = (ch & (fi == s0 + t)) ? old : fold_st;
+        changed |= ch;
+        ap[t * 64] = st;
+        const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
+        const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;
+        const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
+        x0 = nx0; x1 = nx1; x2 = nx2;
+      }
+    }
+    // single-flip passes keep only the QP's first flip over the whole horizon
+    if (single) {
+      int mn = fi;
+#pragma unroll
+      for (int k = L; k < 64; k <<= 1) {
+        const int o = __shfl_xor(mn, k, 64);
+        mn = o < mn ? o : mn;
+      }
+      if (fi < N && fi != mn) {
+        ap[(fi - s0) * 64] = fold_st;
+        changed = false;
+      }
+    }
+    const bool qchanged = (fold(__ballot(changed)) >> sl) & 1ull;
+    if (!qchanged && !done) {
+      done = true;
+      iters = pass + 1;
+    }
+  }
+
+  // ---- output sweep: u* = K x + k from the final gains, x* by the fp64 rollout ----
+  const bool solved = done && !bad;
+  const float nanv = __int_as_float(0x7fc00000);
+  float* uo = uout + (size_t)b * 2 * N;
+  float* xo = xout + (size_t)b * 3 * (N + 1);
+  if (qowner) {
+    xo[0] = solved ? x0g[3 * b + 0] : nanv;
+    xo[1] = solved ? x0g[3 * b + 1] : nanv;
+    xo[2] = solved ? fTH0 : nanv;
+  }
+  const bool want_obj = oo.obj || oo.cost;
+  double J = 0.0, Cr = 0.0;
+  auto qterm = [&](double rx, double ry, double rt, double e0, double e1, double e2) {
+    const double d0 = e0 - rx, d1 = e1 - ry, d2 = e2 - rt;
+    J += 0.5 * (q0 * d0 * d0 + q1 * d1 * d1 + q2 * d2 * d2);
+    const double wx = (ROT ? cs * rx - sn * ry : rx) + X0, wy = (ROT ? sn * rx + cs * ry : ry) + Y0;
+    const double wt = rt + th0;
+    Cr += 0.5 * (q0 * wx * wx + q1 * wy * wy + q2 * wt * wt);
+  };
+  {
+    double x0 = xs0, x1 = xs1, x2 = xs2;
+    for (int t = 0; t < m; t++) {
+      const int i = s0 + t;
+      const double* s = sc + t * 11 * 64;
+      const double K00 = s[0], K01 = s[64], K02 = s[2 * 64], K10 = s[3 * 64], K11 = s[4 * 64];
+      const double K12 = s[5 * 64], k0 = s[6 * 64], k1 = s[7 * 64];
+      const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
+      const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
+      if (want_obj) {
+        qterm(r64[(3 * t) * 64], r64[(3 * t + 1) * 64], r64[(3 * t + 2) * 64], x0, x1, x2);
+        J += 0.5 * (r0 * (u0 - ud0) * (u0 - ud0) + r1 * (u1 - ud1) * (u1 - ud1));
+      }
+      const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
+      const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;
+      const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
+      x0 = nx0; x1 = nx1; x2 = nx2;
+      if (owner) {
+        uo[2 * i] = solved ? (float)u0 : nanv;
+        uo[2 * i + 1] = solved ? (float)u1 : nanv;
+        const double ox = ROT ? cs * x0 - sn * x1 : x0, oy = ROT ? sn * x0 + cs * x1 : x1;
+        xo[3 * i + 3] = solved ? (float)(ox + X0) : nanv;
+        xo[3 * i + 4] = solved ? (float)(oy + Y0) : nanv;
+        xo[3 * i + 5] = solved ? (float)(x2 + th0) : nanv;
+      }
+    }
+    if (want_obj && top) qterm(rNx, rNy, rNt, x0, x1, x2);  // x_N against x_ref[N-1]
+  }
+  if (want_obj) {
+#pragma unroll
+    for (int k = L; k < 64; k <<= 1) {
+      J += __shfl_xor(J, k, 64);
+      Cr += __shfl_xor(Cr, k, 64);
+    }
+    const double Cu = 0.5 * (double)N * (r0 * ud0 * ud0 + r1 * ud1 * ud1);
+    const double dnan = __longlong_as_double(0x7ff8000000000000ll);
+    if (qowner && oo.cost) oo.cost[b] = solved ? J : dnan;
+    if (qowner && oo.obj) oo.obj[b] = solved ? J - Cr - Cu : dnan;
+  }
+  if (qowner) {
+    status_out[b] = bad ? F110QP_NUMERICAL_ID : (done ? F110QP_SOLVED_ID : F110QP_MAX_ITER_ID);
+    if (iters_out) iters_out[b] = bad ? 0 : (done ? iters : max_pass);
+  }
+  if (ws.act) {  // active set of this solution for the next tick (OR over the segments)
+    unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
+    for (int t = 0; t < m; t++) {
+      const int st = ap[t * 64];
+#pragma unroll
+      for (int a = 0; a < 2; a++) {
+        const int va = 2 * (s0 + t) + a, ca = (st >> (2 * a)) & 3;
+        const unsigned long long bit = 1ull << (va & 63);
+        const unsigned long long in0 = va < 64 ? bit : 0ull, in1 = va < 64 ? 0ull : bit;
+        lo0 |= (ca == 1) ? in0 : 0ull;
+        lo1 |= (ca == 1) ? in1 : 0ull;
+        hi0 |= (ca == 2) ? in0 : 0ull;
+        hi1 |= (ca == 2) ? in1 : 0ull;
+      }
+    }
+#pragma unroll
+    for (int k = L; k < 64; k <<= 1) {
+      lo0 |= __shfl_xor(lo0, k, 64);
+      hi0 |= __shfl_xor(hi0, k, 64);
+      lo1 |= __shfl_xor(lo1, k, 64);
+      hi1 |= __shfl_xor(hi1, k, 64);
+    }
+    if (qowner) {
+      ws.act[2 * R * b] = lo0;
+      ws.act[2 * R * b + 1] = hi0;
+      if (R > 1) {
+        ws.act[2 * (R * b + 1)] = lo1;
+        ws.act[2 * (R * b + 1) + 1] = hi1;
+      }
+      if (ws.key) {
+        unsigned* key = ws.key + 4 * b;
+        key[0] = kth; key[1] = kv; key[2] = kd; key[3] = 2u;
+      }
+    }
+  }
+}
+
+template <int S, bool ROT>
+hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
+                             float* uo, float* xo, int* st, int* its, const WarmState& ws,
+                             const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
+  constexpr int L = 64 / S;
+  const int waves = (B + L - 1) / L;
+  const size_t lds = seg_lds_bytes(P.N, S);
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_seg_kernel<S, ROT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((lane_seg_kernel<S, ROT>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr, uo, xo,
+                     st, its, ws, lw.kmax, oo);
+  return hipGetLastError();
+}
+
+}  // namespace f110qp

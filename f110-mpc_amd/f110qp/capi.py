@@ -72,6 +72,7 @@ EXPORTED = (
     "f110qp_solve_grouped_ex_dev",
     "f110qp_select_dev",
     "f110qp_backend_info",
+    "f110qp_lane_segments",
 )
 SCRATCH_NAMES = {0: "none (wave back end)", 1: "LDS fp64", 2: "LDS fp32", 3: "HBM fp64", 4: "HBM fp32"}
 
@@ -139,6 +140,7 @@ def load():
     L.f110qp_solve_grouped_ex_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 7
     L.f110qp_select_dev.argtypes = [C.c_int, fp, C.c_int, fp, fp, fp, fp, fp]
     L.f110qp_backend_info.argtypes = [C.c_void_p, C.c_int, C.c_int] + [C.POINTER(C.c_int)] * 3
+    L.f110qp_lane_segments.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
     L.f110qp_warm_reset.argtypes = [C.c_void_p]
     L.f110qp_qp_dims.argtypes = [C.c_int] + [C.POINTER(C.c_int)] * 4
@@ -226,6 +228,13 @@ class Solver:
         _check(self.lib.f110qp_backend_info(self._h, int(batch), int(grouped), *[C.byref(x) for x in v]),
                "f110qp_backend_info")
         return tuple(x.value for x in v)
+
+    def lane_segments(self, batch: int) -> int:
+        """Horizon segments per QP of a solve call of `batch` QPs (f110qp_lane_segments): 1, or
+        2 / 4 / 8 when the lane back end runs the partitioned Riccati (lane_seg_kernel.h)."""
+        v = C.c_int()
+        _check(self.lib.f110qp_lane_segments(self._h, int(batch), C.byref(v)), "f110qp_lane_segments")
+        return v.value
 
     def solve(self, x0, u_lin, x_ref, halfspace=None, objective=False):
         """Host arrays in, host arrays out (synchronous). Returns (u[B,N,2], x[B,N+1,3],

@@ -201,6 +201,11 @@ int f110qp_select_dev(int batch, const int* group, int num_groups, const double*
 int f110qp_backend_info(f110qp_ctx* ctx, int batch, int grouped, int* backend, int* qps_per_wave,
                         int* scratch);
 
+/* Horizon segments per QP of that launch: 1, or S = 2 / 4 / 8 when the lane back end splits each
+ * QP's horizon over S lanes (partitioned Riccati; batches too small to give every SIMD a wave of
+ * distinct QPs). The result is the exact optimum either way. */
+int f110qp_lane_segments(f110qp_ctx* ctx, int batch, int* segments);
+
 /* Forget the warm-start state of every slot (the next call solves cold). */
 int f110qp_warm_reset(f110qp_ctx* ctx);
 

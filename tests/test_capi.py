@@ -149,7 +149,10 @@ def test_backend_info_resolves_auto_and_scratch(capi):
     assert s20.backend_info(65536) == (capi.BACKEND_LANE, 64, 4)
     s40 = capi.Solver(capi.default_config(40))
     assert s40.backend_info(capi.LANE_MIN_BATCH_WIDE - 1)[0] == capi.BACKEND_WAVE
-    assert s40.backend_info(8192, grouped=True) == (capi.BACKEND_LANE, 32, 1)
+    # small batches split every QP's horizon over S lanes (lane_seg_kernel.h): 64 / S QPs per wave
+    assert s40.backend_info(8192, grouped=True) == (capi.BACKEND_LANE, 8, 1)
+    assert s40.lane_segments(8192) == 8 and s20.lane_segments(4096) == 4
+    assert s20.lane_segments(65536) == 1 and s20.lane_segments(1024) == 1  # 1,024: wave back end
     assert s40.backend_info(65536, grouped=True) == (capi.BACKEND_LANE, 64, 4)
     sg = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE))
     assert sg.backend_info(65536)[0] == capi.BACKEND_WAVE

@@ -1,0 +1,169 @@
+"""Parity of the partitioned-horizon lane kernel (csrc/lane_seg_kernel.h: each QP's horizon split
+over S = 2 / 4 / 8 lanes, a Riccati recursion over the segment ends) with the exact optimum of the
+CPU oracle, through the C ABI. F110QP_LANE_SEG forces S (1 = the sequential lane_kernel.h).
+Tolerance: the north star's 1e-4 relative; observed at the fp32 output rounding (~1e-7)."""
+import numpy as np
+import pytest
+
+from f110qp import workload
+
+from test_gpu_parity import TOL, check, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _lane(capi, N, **cfg):
+    return capi.Solver(capi.default_config(N, backend=capi.BACKEND_LANE, **cfg))
+
+
+@pytest.mark.parametrize("S,N", [(2, 2), (2, 10), (4, 20), (2, 30), (8, 40), (4, 40), (2, 40), (8, 48), (4, 4), (8, 16)])
+def test_segments_horizons(oracle, capi, monkeypatch, S, N):
+    """Every segment count on horizons it divides (segments of 1.. 24 stages), many active bounds
+    on both faces, batch not a multiple of the QPs per wave."""
+    monkeypatch.setenv("F110QP_LANE_SEG", str(S))
+    w = workload.make_batch(1000, N, seed=9100 + 10 * S + N, heading="true", lateral=1.5, steer_range=1.0)
+    s = _lane(capi, N)
+    assert s.lane_segments(1000) == (S if N // S >= 2 else 1)
+    s.close()
+    u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
+    assert (st == capi.SOLVED).all()
+
+
+@pytest.mark.parametrize("rot", ["0", "1"])
+@pytest.mark.parametrize("S", ["2", "4"])
+def test_segments_general_frame_far_origin(oracle, capi, monkeypatch, rot, S):
+    """Heading frame (q0 == q1) and general frame (F110QP_LANE_ROT=0), headings all round the
+    circle, 1 km from the origin."""
+    monkeypatch.setenv("F110QP_LANE_SEG", S)
+    monkeypatch.setenv("F110QP_LANE_ROT", rot)
+    N, B = 20, 1500
+    w = workload.make_batch(B, N, seed=6161, heading="true", lateral=1.5, steer_range=1.0)
+    w["x0"][:, 2] = np.random.default_rng(5).uniform(-np.pi, np.pi, B).astype(np.float32)
+    w["x0"][:, :2] += np.float32(1000.0)
+    w["x_ref"][:, :, :2] += np.float32(1000.0)
+    check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
+
+
+def test_segments_custom_weights(oracle, capi, monkeypatch):
+    """q0 != q1 (general frame), other R, u_des inside the box, narrow bounds."""
+    monkeypatch.setenv("F110QP_LANE_SEG", "4")
+    N = 20
+    over = dict(q=[3.0, 7.0, 2.0], r=[0.5, 1.5], u_des=[3.7, 0.05], u_min=[3.5, -0.2], u_max=[4.0, 0.2])
+    w = workload.make_batch(640, N, seed=882, lateral=0.7)
+    check(oracle, capi, N, w, backend=capi.BACKEND_LANE, **over)
+
+
+@pytest.mark.parametrize("kmax,S,N", [("0", "4", 20), ("1", "4", 20), ("0", "8", 40), ("2", "2", 40)])
+def test_segments_single_flip(oracle, capi, monkeypatch, kmax, S, N):
+    """Past kmax PDAS passes a QP flips only its first violation over the WHOLE horizon (the min
+    over its segment lanes; the other segments undo theirs): exact results, more passes."""
+    monkeypatch.setenv("F110QP_LANE_SEG", S)
+    monkeypatch.setenv("F110QP_LANE_KMAX", kmax)
+    w = workload.make_batch(1200, N, seed=992 + N, heading="true", lateral=1.5, steer_range=1.0)
+    u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
+    monkeypatch.setenv("F110QP_LANE_SEG", "1")
+    s = _lane(capi, N)
+    _, _, _, it_seq = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    # the same single-flip iterates as the sequential kernel (pass counts agree)
+    assert np.abs(it.astype(int) - it_seq.astype(int)).max() <= 1
+    monkeypatch.delenv("F110QP_LANE_KMAX")
+    monkeypatch.setenv("F110QP_LANE_SEG", S)
+    s = _lane(capi, N)
+    _, _, _, it_pdas = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    assert it.max() > it_pdas.max()
+
+
+@pytest.mark.parametrize("S", ["2", "4", "8"])
+def test_segments_agree_with_sequential(capi, monkeypatch, S):
+    """Same PDAS iterates as lane_kernel.h (pass counts equal on all but rounding ties), same
+    status, solutions within 1e-7."""
+    N, B = 40, 2048
+    w = workload.make_batch(B, N, seed=2222, heading="true", lateral=1.2, steer_range=0.8)
+    out = {}
+    for seg in ("1", S):
+        monkeypatch.setenv("F110QP_LANE_SEG", seg)
+        s = _lane(capi, N)
+        out[seg] = s.solve(w["x0"], w["u_lin"], w["x_ref"], objective=True)
+        s.close()
+    a, b = out["1"], out[S]
+    np.testing.assert_array_equal(a[2], b[2])
+    assert (a[3] != b[3]).mean() < 0.01
+    assert rel_err(b[0], a[0].astype(np.float64)).max() <= 1e-6
+    assert rel_err(b[1], a[1].astype(np.float64)).max() <= 1e-6
+    np.testing.assert_allclose(b[4], a[4], rtol=1e-9, atol=1e-9 * np.abs(a[4]).max())
+    np.testing.assert_allclose(b[5], a[5], rtol=1e-9, atol=1e-12)
+
+
+def test_segments_objective(oracle, capi, monkeypatch):
+    """obj / cost outputs (the segment lanes' partial sums reduced across the QP) against the
+    oracle's objective of its exact optimum."""
+    monkeypatch.setenv("F110QP_LANE_SEG", "4")
+    N, B = 40, 500
+    w = workload.make_batch(B, N, seed=1717, heading="true", lateral=1.0, steer_range=0.6)
+    s = _lane(capi, N)
+    u, x, st, it, obj, cost = s.solve(w["x0"], w["u_lin"], w["x_ref"], objective=True)
+    s.close()
+    prm = oracle.params(N)
+    ur, xr, sr, obr = oracle.solve_batch(prm, w["x0"], w["u_lin"], w["x_ref"], objective=True)
+    np.testing.assert_array_equal(st, sr)
+    np.testing.assert_allclose(obj, obr, rtol=1e-6, atol=1e-6)
+    cr = oracle.tracking_cost(prm, ur, xr, w["x_ref"])
+    assert (np.abs(cost - cr) <= 1e-6 * np.maximum(1.0, cr)).all(), np.abs(cost - cr).max()
+    assert np.isfinite(obj).all() and (cost >= 0).all()
+
+
+def test_segments_warm_closed_loop(oracle, capi, monkeypatch):
+    """C5 as a closed loop on the segmented kernel (auto picks S = 4 at 4,096 x N = 20): every tick
+    at the exact optimum, warm passes no more than cold on average."""
+    N, B, T = 20, 4096, 6
+    prm = oracle.params(N)
+    ref = []
+
+    def solve(x0, ul, xr):
+        u, x, st = oracle.solve_batch(prm, x0, ul, xr)
+        ref.append((u, x, st))
+        return u
+
+    ticks = workload.closed_loop_stream(solve, B, N, T, seed=56)
+    warm = _lane(capi, N, warm_start=1)
+    assert warm.lane_segments(B) == 4
+    for t, w in enumerate(ticks):
+        u, x, st, it = warm.solve(w["x0"], w["u_lin"], w["x_ref"])
+        ur, xr, sr = ref[t]
+        np.testing.assert_array_equal(st, sr)
+        assert rel_err(u, ur).max() <= TOL and rel_err(x, xr).max() <= TOL, t
+    warm.close()
+
+
+def test_segments_non_finite(oracle, capi, monkeypatch):
+    """NaN / inf inputs: NUMERICAL and NaN outputs on every segment of those QPs only."""
+    monkeypatch.setenv("F110QP_LANE_SEG", "4")
+    N, B = 20, 777
+    w = workload.make_batch(B, N, seed=1414)
+    bad = {3: ("x_ref", (3, 17, 0), np.nan), 70: ("x0", (70, 2), np.inf), 130: ("u_lin", (130, 1), np.nan),
+           776: ("x_ref", (776, N - 1, 2), np.nan)}
+    for b, (k, idx, v) in bad.items():
+        w[k][idx] = v
+    s = _lane(capi, N)
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    badi = np.array(sorted(bad))
+    assert (st[badi] == capi.NUMERICAL).all()
+    assert np.isnan(u[badi]).all() and np.isnan(x[badi]).all()
+    good = np.setdiff1d(np.arange(B), badi)[::7]
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][good], w["u_lin"][good], w["x_ref"][good])
+    assert (st[good] == capi.SOLVED).all()
+    assert rel_err(u[good], ur).max() <= TOL and rel_err(x[good], xr).max() <= TOL
+
+
+def test_segments_degenerate_bound(oracle, capi, monkeypatch):
+    """u_des on the speed bound with Q = 0: zero multipliers; the flip tolerances hold on the
+    segmented kernel too."""
+    monkeypatch.setenv("F110QP_LANE_SEG", "4")
+    N = 20
+    for q in ([0.0, 0.0, 0.0], [1e-9, 1e-9, 0.0]):
+        w = workload.make_batch(700, N, seed=4500, heading="true", lateral=0.0, steer_range=0.0)
+        u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE, tol=2e-6, q=q)
+        assert (st == capi.SOLVED).all()
