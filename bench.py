@@ -53,6 +53,10 @@ FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) pea
 FP64_PEAK_TFLOPS = 78.6     # MI355X spec FP64 vector; tools/microbench/latency.hip measures the
                             # matching issue rate (one wave64 fp64 FMA per 4 cycles per SIMD)
 LANE_FLOPS_PER_STAGE = 290  # fp64 flops per stage and pass of lane_kernel (ISA count)
+# lane_seg_kernel (partitioned horizon): per stage and pass the backward stage with the segment's
+# closed-loop map (160 fp64 instructions), the feed-forward refresh (16) and the forward (35);
+# ~2.5 flops per instruction as above, the S - 1 segment steps (~200 fp64 each) spread per stage
+SEG_FLOPS_PER_STAGE = 530
 
 
 def bytes_per_qp(N: int, gap: bool, warm: bool = False, backend: str = "wave") -> int:
@@ -294,8 +298,8 @@ def main():
                     help="grouped solve (one W = H^-1 per 120-candidate scenario, f110qp_solve_grouped_dev); "
                          "auto = on for c4")
     ap.add_argument("--backend", default="auto", choices=["auto", "wave", "lane"],
-                    help="solver back end (auto: lane-per-QP for box-only batches >= capi.LANE_MIN_BATCH = 3072 "
-                         "at N <= 32, >= capi.LANE_MIN_BATCH_WIDE = 768 at N > 32; f110qp_backend_info)")
+                    help="solver back end (auto: lane-per-QP for box-only batches >= capi.LANE_MIN_BATCH = 1536 "
+                         "at N <= 32, >= capi.LANE_MIN_BATCH_WIDE = 1 at N > 32; f110qp_backend_info)")
     args = ap.parse_args()
 
     import torch
@@ -404,6 +408,7 @@ def main():
     # the launch this call makes, as the library resolves it (back end, QPs per wave, scratch)
     eff, lane_qpw, lane_scr = solver.backend_info(Bper, grouped)
     be_name = "lane" if eff == capi.BACKEND_LANE else "wave"
+    lane_seg = solver.lane_segments(Bper) if be_name == "lane" else 1
     if be_name == "lane":
         dtype = "fp64" if lane_scr in (1, 3) else "fp64 (fp32 Riccati-gain scratch in " + (
             "LDS)" if lane_scr == 2 else "HBM)")
@@ -514,7 +519,8 @@ def main():
     # active-set size ~ iterations for an add-only run; use iterations as the upper bound
     if be_name == "lane":
         # Riccati + forward + adjoint sweeps: (active-set changes + 1) passes over N stages
-        fpq = LANE_FLOPS_PER_STAGE * N * (float(itn.mean()) + 1.0)
+        fpq = (LANE_FLOPS_PER_STAGE if lane_seg == 1 else SEG_FLOPS_PER_STAGE + 500.0 * (lane_seg - 1) / N * lane_seg) \
+            * N * (float(itn.mean()) + 1.0)
         cpeak, cname = FP64_PEAK_TFLOPS, "fp64_compute"
     else:
         # pivots >= bounds active at the solution (each entered the active set once)
@@ -550,7 +556,8 @@ def main():
             "warm_start": bool(warm),
             "backend": {"wave": "wave-per-QP (condensed, PDAS/GI)", "lane": "lane-per-QP (Riccati/PDAS fp64)"}[be_name]
                        + (" grouped: one W = H^-1 per scenario" if grouped and be_name == "wave" else ""),
-            **({"lane_qps_per_wave": lane_qpw, "lane_scratch": capi.SCRATCH_NAMES[lane_scr]}
+            **({"lane_qps_per_wave": lane_qpw, "lane_scratch": capi.SCRATCH_NAMES[lane_scr],
+                "lane_segments": lane_seg}
                if be_name == "lane" else {}),
             "parallelism": f"independent QP shards x{world} (no collective)"
                            + (f", scenario-aligned ({GROUP}) split of one global batch" if strong else ""),
@@ -578,13 +585,18 @@ def main():
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
             "kernel": {"wave": "f110qp::solve_kernel",
-                       "lane": "f110qp::lane_kernel (the only launch of the step)"}[be_name],
+                       "lane": ("f110qp::lane_kernel" if lane_seg == 1 else
+                                f"f110qp::lane_seg_kernel<{lane_seg}> (partitioned horizon)")
+                               + " (the only launch of the step)"}[be_name],
             "kernel_ms_per_launch": kms,
             "algorithmic_bytes_per_qp": bpq,
             cname: {"achieved": achieved_tf, "peak": cpeak, "unit": "TFLOP/s",
                     "frac": achieved_tf / cpeak, "flops_per_qp": fpq},
             "note": ("lane kernel: fp64 VALU-issue and scratch-latency bound (Riccati sweeps, 64 QPs per "
-                     "wave); traffic = PMC HBM bytes incl. the Riccati scratch" if be_name == "lane" else
+                     "wave); traffic = PMC HBM bytes incl. the Riccati scratch" if be_name == "lane" and lane_seg == 1 else
+                     f"partitioned-horizon lane kernel: one QP per {lane_seg} lanes, latency-bound by the slowest "
+                     "QP's PDAS passes x (N/S stages + S-1 segment steps); scratch in LDS, HBM = inputs/outputs"
+                     if be_name == "lane" else
                      "wave kernel: latency-bound (serial active-set chain per wave); neither HBM nor FP32 "
                      "peak binds"),
         },

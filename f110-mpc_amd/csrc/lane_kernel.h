@@ -138,43 +138,48 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
   const int n3 = 3 * N;
 
   // ---- stage the wave's reference paths (nq rows of 3S floats, the first 3N of each used) ---
-  // Linear, coalesced sweep over the rows' first 3N entries (element e -> QP e / 3N, entry
-  // e % 3N), written transposed to LDS. All loads of a chunk per lane are issued before the
-  // first LDS write, so the wave waits for HBM once per chunk, not once per load. A non-finite
-  // entry flags its QP in a bit mask (one bit per QP of the wave, OR-ed over the lanes).
-  unsigned long long badq = 0ull;
+  // Linear, coalesced sweep over the rows' first 3N entries (element e = q 3N + c -> stg[c L + q],
+  // transposed). (q, c) advance by 64 elements per step without a division, every load reads a
+  // valid address (clamped) and only the last chunk predicates its stores, so the full chunks
+  // have no EXEC-masked region: ~18 instructions per element instead of ~50 (ISA). All loads of
+  // a chunk per lane are issued before the first LDS write.
   {
     const int S3 = 3 * P.xr_stride;  // floats per QP in x_ref (>= 3N)
     const int tot = nq * n3;
     const float* src = xrg + (size_t)b0 * S3;
-    const float rn3 = 1.0f / (float)n3;
+    const int dq = 64 / n3, dc = 64 - dq * n3;
+    int q = lane / n3, c = lane - (lane / n3) * n3;
+    const int last_off = (nq - 1) * S3 + (n3 - 1);
     constexpr int kChunk = 8;
     for (int e0 = 0; e0 < tot; e0 += kChunk * 64) {
       float vbuf[kChunk];
       int dst[kChunk];
 #pragma unroll
       for (int j = 0; j < kChunk; j++) {
-        const int e = e0 + j * 64 + lane;
-        int q = (int)((float)e * rn3);
-        q -= (q * n3 > e) ? 1 : 0;
-        q += ((q + 1) * n3 <= e) ? 1 : 0;
-        const int c = e - q * n3;
-        dst[j] = (e < tot) ? c * L + q : -1;
-        vbuf[j] = (e < tot) ? src[(size_t)q * S3 + c] : 0.f;
+        const bool in = e0 + j * 64 + lane < tot;
+        dst[j] = in ? c * L + q : -1;
+        vbuf[j] = src[in ? q * S3 + c : last_off];
+        q += dq;
+        c += dc;
+        const bool wrap = c >= n3;
+        c -= wrap ? n3 : 0;
+        q += wrap ? 1 : 0;
       }
+      if (e0 + kChunk * 64 <= tot) {  // wave-uniform
 #pragma unroll
-      for (int j = 0; j < kChunk; j++) {
-        if (dst[j] >= 0) stg[dst[j]] = vbuf[j];
-        if (!isfinite(vbuf[j])) badq |= 1ull << (dst[j] & (L - 1));  // q = dst mod L
+        for (int j = 0; j < kChunk; j++) stg[dst[j]] = vbuf[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < kChunk; j++)
+          if (dst[j] >= 0) stg[dst[j]] = vbuf[j];
       }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {  // OR over the wave (64-bit shuffles)
-      const unsigned lo = __shfl_xor((unsigned)badq, o), hi = __shfl_xor((unsigned)(badq >> 32), o);
-      badq |= ((unsigned long long)hi << 32) | lo;
     }
     __syncthreads();
   }
+  // a non-finite reference entry flags the QP: each lane scans its QP's staged row (~10
+  // instructions per entry; a ballot per staged element measured more at C4 and c2_big sizes)
+  bool nonfin = false;
+  for (int e = 0; e < n3; e++) nonfin |= !isfinite(stg[e * L + slot]);
 
   // ---- per-lane QP data (Model::Linearize, model.cpp:30-59; fp64 of the float inputs) ----
   const double X0 = (double)x0g[3 * b + 0], Y0 = (double)x0g[3 * b + 1];
@@ -269,16 +274,18 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
     }
     // (a cold start from the free set beats seeding the inputs whose u_des sits on a bound:
     // measured +0.5 PDAS passes per QP with the seed on the C2/C4 workloads)
+    // stage i's two bits sit at bit 2i of the 128-bit (row 1 : row 0) masks: shifted out two at a
+    // time (per input: 1 lower, 2 upper, 0 free; the lower bound wins)
+    unsigned long long lw = lo0, hw = hi0;
     for (int i = 0; i < N; i++) {
-      int st = 0;
-#pragma unroll
-      for (int a = 0; a < 2; a++) {
-        const int va = 2 * i + a;
-        const unsigned long long l = va < 64 ? lo0 : lo1, h = va < 64 ? hi0 : hi1;
-        const int ca = ((l >> (va & 63)) & 1ull) ? 1 : (((h >> (va & 63)) & 1ull) ? 2 : 0);
-        st |= ca << (2 * a);
+      if (i == 32) {
+        lw = lo1;
+        hw = hi1;
       }
-      ap[i * L] = st;
+      const unsigned l2 = (unsigned)lw & 3u, h2 = (unsigned)hw & 3u & ~l2;
+      ap[i * L] = (int)((l2 & 1u) | ((h2 & 1u) << 1) | ((l2 & 2u) << 1) | ((h2 & 2u) << 2));
+      lw >>= 2;
+      hw >>= 2;
     }
   }
   // recentred (ROT: rotated) reference of stage i from the float staging
@@ -316,8 +323,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
   // non-finite data -> F110QP_NUMERICAL with NaN outputs (e.g. the planning stage's NaN x_ref
   // of a scenario without a valid candidate, where the reference skips MPC::Update). Such a
   // lane keeps sweeping (NaN) in lock step but never holds the wave back.
-  const bool bad = !(isfinite(X0) && isfinite(Y0) && isfinite(th0) && isfinite(v) && isfinite(d)) ||
-                   ((badq >> slot) & 1ull);
+  const bool bad = !(isfinite(X0) && isfinite(Y0) && isfinite(th0) && isfinite(v) && isfinite(d)) || nonfin;
   bool done = bad;
   int iters = 0;
 #ifdef F110QP_STAMPS
@@ -693,16 +699,15 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
   if (owner && ws.act) {  // active set of this solution for the next tick
     unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
     for (int i = 0; i < N; i++) {
-      const int st = ap[i * L];
-#pragma unroll
-      for (int a = 0; a < 2; a++) {
-        const int va = 2 * i + a, ca = (st >> (2 * a)) & 3;
-        const unsigned long long bit = 1ull << (va & 63);
-        const unsigned long long in0 = va < 64 ? bit : 0ull, in1 = va < 64 ? 0ull : bit;
-        lo0 |= (ca == 1) ? in0 : 0ull;
-        lo1 |= (ca == 1) ? in1 : 0ull;
-        hi0 |= (ca == 2) ? in0 : 0ull;
-        hi1 |= (ca == 2) ? in1 : 0ull;
+      const unsigned st = (unsigned)ap[i * L];
+      const unsigned long long l2 = (st & 1u) | ((st >> 1) & 2u), h2 = ((st >> 1) & 1u) | ((st >> 2) & 2u);
+      const int sh = 2 * (i & 31);
+      if (i < 32) {
+        lo0 |= l2 << sh;
+        hi0 |= h2 << sh;
+      } else {
+        lo1 |= l2 << sh;
+        hi1 |= h2 << sh;
       }
     }
     ws.act[2 * R * b] = lo0;

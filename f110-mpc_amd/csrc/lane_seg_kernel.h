@@ -47,6 +47,18 @@
 
 namespace f110qp {
 
+// Diagnostic build only (-DF110QP_STAMPS on lane_seg_inst.hip): per-wave cycles of the setup, each
+// pass phase and the output, read back with f110qp_read_seg_stamps(). Never in the shipped library.
+#ifdef F110QP_STAMPS
+constexpr int kSegStampSlots = 8;
+__device__ unsigned long long g_sstamps[4096 * kSegStampSlots];
+#define SSTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define SACC(acc, since) acc += __builtin_amdgcn_s_memtime() - (since)
+#else
+#define SSTAMP(var)
+#define SACC(acc, since)
+#endif
+
 // LDS bytes per wave of the segmented kernel for horizon N split into S segments
 constexpr size_t seg_lds_bytes(int N, int S) { return (size_t)(N / S) * 64 * (3 * 8 + 4 + 11 * 8); }
 
@@ -78,52 +90,61 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const bool top = seg == S - 1;
   const int up = (lane + L) & 63, dn = (lane - L) & 63;  // same QP, segment + 1 / - 1 (ring)
 
+  SSTAMP(t_start);
+#ifdef F110QP_STAMPS
+  unsigned long long acc_bw = 0, acc_dual = 0, acc_ref = 0, acc_fw = 0, t_setup = 0, npass = 0;
+#endif
   double* const r64 = seg_smem + lane;                                   // [3m][64]
   int* const ap = reinterpret_cast<int*>(seg_smem + 3 * m * 64) + lane;  // [m][64]
   double* const sc = seg_smem + 3 * m * 64 + m * 32 + lane;              // [m][11][64]
 
+  // per-QP inputs and the warm-start key, issued before the staging loads so that both share
+  // one HBM round trip
+  const float fX0 = x0g[3 * b + 0], fY0 = x0g[3 * b + 1], fTH0 = x0g[3 * b + 2];
+  const float fv = ulg[2 * b + 0], fd = ulg[2 * b + 1];
+  unsigned key0 = 0u, key1 = 0u, key2 = 0u, key3 = 0u;
+  if (ws.act && ws.key) {
+    const unsigned* key = ws.key + 4 * b;
+    key0 = key[0]; key1 = key[1]; key2 = key[2]; key3 = key[3];
+  }
   // ---- stage the wave's reference paths (float, [3N][L]) into the scratch region ----
-  unsigned long long badq = 0ull;
+  // Element e = q 3N + c of the wave's nq rows (row stride 3 xr_stride in HBM) goes to
+  // stg[c L + q]. (q, c) advance by 64 elements per step without a division, every load reads a
+  // valid address (clamped) and every store lands (past the staged rows for e >= tot), so the
+  // loop has no EXEC-masked region: ~11 instructions per element instead of ~50 (ISA).
   {
     float* stg = reinterpret_cast<float*>(seg_smem + 3 * m * 64 + m * 32);
-    const int n3 = 3 * N;
-    const int S3 = 3 * P.xr_stride;
-    const int tot = nq * n3;
+    const int n3 = 3 * N, S3 = 3 * P.xr_stride, tot = nq * n3;
     const float* src = xrg + (size_t)b0 * S3;
-    const float rn3 = 1.0f / (float)n3;
-    constexpr int kChunk = 8;
+    const int dq = 64 / n3, dc = 64 - dq * n3;
+    int q = lane / n3, c = lane - (lane / n3) * n3;
+    const int junk = n3 * L + lane;                  // inside the scratch rows, never read
+    const int last_off = (nq - 1) * S3 + (n3 - 1);  // a valid element for the clamped loads
+    constexpr int kChunk = 16;  // C5 and the C4 shard stage 960 floats per wave: one round trip
     for (int e0 = 0; e0 < tot; e0 += kChunk * 64) {
       float vbuf[kChunk];
       int dst[kChunk];
 #pragma unroll
       for (int j = 0; j < kChunk; j++) {
-        const int e = e0 + j * 64 + lane;
-        int q = (int)((float)e * rn3);
-        q -= (q * n3 > e) ? 1 : 0;
-        q += ((q + 1) * n3 <= e) ? 1 : 0;
-        const int c = e - q * n3;
-        dst[j] = (e < tot) ? c * L + q : -1;
-        vbuf[j] = (e < tot) ? src[(size_t)q * S3 + c] : 0.f;
+        const bool in = e0 + j * 64 + lane < tot;
+        dst[j] = in ? c * L + q : junk;
+        vbuf[j] = src[in ? q * S3 + c : last_off];
+        q += dq;
+        c += dc;
+        const bool wrap = c >= n3;
+        c -= wrap ? n3 : 0;
+        q += wrap ? 1 : 0;
       }
 #pragma unroll
-      for (int j = 0; j < kChunk; j++) {
-        if (dst[j] >= 0) stg[dst[j]] = vbuf[j];
-        if (!isfinite(vbuf[j])) badq |= 1ull << (dst[j] & (L - 1));
-      }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const unsigned lo = __shfl_xor((unsigned)badq, o), hi = __shfl_xor((unsigned)(badq >> 32), o);
-      badq |= ((unsigned long long)hi << 32) | lo;
+      for (int j = 0; j < kChunk; j++) stg[dst[j]] = vbuf[j];
     }
     __syncthreads();
   }
 
   // ---- per-lane QP data (Model::Linearize, model.cpp:30-59), as lane_kernel.h ----
-  const double X0 = (double)x0g[3 * b + 0], Y0 = (double)x0g[3 * b + 1];
-  const float fTH0 = x0g[3 * b + 2];
+  const double X0 = (double)fX0, Y0 = (double)fY0;
   const double th0 = (double)fTH0;
-  const double v = (double)ulg[2 * b + 0], d = (double)ulg[2 * b + 1];
+  const double v = (double)fv, d = (double)fd;
   const double dt = (double)P.dt;
   const double Lw = (double)0.3302f;
   double sn, cs, sd, cd;
@@ -148,16 +169,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const double gtol0 = gt * (1.0 + r0 * (1.0 + fabs(lb0) + fabs(ub0)));
   const double gtol1 = gt * (1.0 + r1 * (1.0 + fabs(lb1) + fabs(ub1)));
 
-  // references of the lane's stages: recentred (ROT: rotated) fp64, lane-major
+  // references of the lane's stages: recentred (ROT: rotated) fp64, lane-major; a non-finite
+  // entry flags the QP (one ballot folded over its segment lanes)
+  bool nonfin = false;
   {
     const float* stg = reinterpret_cast<const float*>(seg_smem + 3 * m * 64 + m * 32);
     for (int t = 0; t < m; t++) {
       const int i = s0 + t;
-      const double dx = (double)stg[(3 * i + 0) * L + slot] - X0;
-      const double dy = (double)stg[(3 * i + 1) * L + slot] - Y0;
+      const float fx = stg[(3 * i + 0) * L + slot], fy = stg[(3 * i + 1) * L + slot];
+      const float ft = stg[(3 * i + 2) * L + slot];
+      nonfin |= !(isfinite(fx) && isfinite(fy) && isfinite(ft));
+      const double dx = (double)fx - X0, dy = (double)fy - Y0;
       r64[(3 * t + 0) * 64] = ROT ? cs * dx + sn * dy : dx;
       r64[(3 * t + 1) * 64] = ROT ? cs * dy - sn * dx : dy;
-      r64[(3 * t + 2) * 64] = (double)stg[(3 * i + 2) * L + slot] - th0;
+      r64[(3 * t + 2) * 64] = (double)ft - th0;
     }
     __syncthreads();  // the staging region becomes the Riccati scratch
   }
@@ -168,15 +193,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 
   // warm start: previous tick's active bounds when the slot's (theta0, v, steer) bits repeat
   const int R = (2 * N + 63) / 64;
-  const unsigned kth = __float_as_uint(fTH0), kv = __float_as_uint(ulg[2 * b + 0]);
-  const unsigned kd = __float_as_uint(ulg[2 * b + 1]);
+  const unsigned kth = __float_as_uint(fTH0), kv = __float_as_uint(fv), kd = __float_as_uint(fd);
   {
     unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
-    bool hit = false;
-    if (ws.act && ws.key) {
-      const unsigned* key = ws.key + 4 * b;
-      hit = key[3] != 0u && key[0] == kth && key[1] == kv && key[2] == kd;
-    }
+    const bool hit = ws.act && ws.key && key3 != 0u && key0 == kth && key1 == kv && key2 == kd;
     if (hit) {
       lo0 = ws.act[2 * R * b];
       hi0 = ws.act[2 * R * b + 1];
@@ -185,26 +205,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         hi1 = ws.act[2 * (R * b + 1) + 1];
       }
     }
-    for (int t = 0; t < m; t++) {
-      const int i = s0 + t;
-      int st = 0;
-#pragma unroll
-      for (int a = 0; a < 2; a++) {
-        const int va = 2 * i + a;
-        const unsigned long long l = va < 64 ? lo0 : lo1, h = va < 64 ? hi0 : hi1;
-        const int ca = ((l >> (va & 63)) & 1ull) ? 1 : (((h >> (va & 63)) & 1ull) ? 2 : 0);
-        st |= ca << (2 * a);
-      }
-      ap[t * 64] = st;
+    // the lane's 2m mask bits start at bit 2 s0 of the 128-bit pair (hi word : lo word)
+    const int sh = 2 * s0;
+    auto window = [&](unsigned long long w0, unsigned long long w1) {
+      return sh >= 64 ? (w1 >> (sh - 64)) : (sh == 0 ? w0 : ((w0 >> sh) | (w1 << (64 - sh))));
+    };
+    const unsigned long long lw = window(lo0, lo1), hw = window(hi0, hi1);
+    for (int t = 0; t < m; t++) {  // per input: 1 lower, 2 upper, 0 free; the lower bound wins
+      const unsigned l2 = (unsigned)(lw >> (2 * t)) & 3u, h2 = (unsigned)(hw >> (2 * t)) & 3u & ~l2;
+      ap[t * 64] = (int)((l2 & 1u) | ((h2 & 1u) << 1) | ((l2 & 2u) << 1) | ((h2 & 2u) << 2));
     }
   }
-
-  const bool bad = !(isfinite(X0) && isfinite(Y0) && isfinite(th0) && isfinite(v) && isfinite(d)) ||
-                   ((badq >> slot) & 1ull);
-  bool done = bad;
-  int iters = 0;
-  // the segment's start state of the current pass (kept for the output sweep)
-  double xs0 = 0.0, xs1 = 0.0, xs2 = 0.0;
 
   // wave-uniform fold of a ballot over the QP's S lanes: bit sl set if any segment's bit is
   auto fold = [&](unsigned long long mk) {
@@ -212,11 +223,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     for (int k = L; k < 64; k <<= 1) mk |= mk >> k;
     return mk;
   };
+  const bool bad = !(isfinite(X0) && isfinite(Y0) && isfinite(th0) && isfinite(v) && isfinite(d)) ||
+                   ((fold(__ballot(nonfin)) >> sl) & 1ull);
+  bool done = bad;
+  int iters = 0;
+  // the segment's start state of the current pass (kept for the output sweep)
+  double xs0 = 0.0, xs1 = 0.0, xs2 = 0.0;
+
 
   const int max_pass = P.max_iter > kmax ? P.max_iter : kmax;
+#ifdef F110QP_STAMPS
+  t_setup = __builtin_amdgcn_s_memtime() - t_start;
+#endif
   for (int pass = 0; pass < max_pass; pass++) {
     if (__ballot(!done) == 0ull) break;
     const bool single = pass >= kmax;
+#ifdef F110QP_STAMPS
+    npass++;
+#endif
+    SSTAMP(t_bw);
     // ---- 1. backward over the segment: Riccati + the closed-loop map (Phi, psi, Gam) ----
     double P00 = top ? q0 : 0.0, P01 = 0.0, P02 = 0.0, P11 = top ? q1 : 0.0, P12 = 0.0;
     double P22 = top ? q2 : 0.0;
@@ -322,6 +347,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         F02 = n02; F12 = n12; F22 = n22;
       }
     }
+    SACC(acc_bw, t_bw);
+    SSTAMP(t_dual);
     // ---- 2. the segment ends: Riccati over the segments, then lam_j, x_s^(j) forward ----
     // the top segment hands (P, a) up the chain and x_e = 0 round the ring to segment 0
     if (top) {
@@ -405,6 +432,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       lm1 = top ? 0.0 : T10 * xs0 + T11 * xs1 + T12 * xs2 + t1;
       lm2 = top ? 0.0 : T20 * xs0 + T21 * xs1 + T22 * xs2 + t2;
     }
+    SACC(acc_dual, t_dual);
+    SSTAMP(t_ref);
     // ---- 3. refresh: the lam-part of the feed-forward, backward over the segment ----
     double pl0 = lm0, pl1 = lm1, pl2 = lm2;
     if constexpr (S > 1) {
@@ -431,6 +460,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         pl0 = n0; pl1 = n1;
       }
     }
+    SACC(acc_ref, t_ref);
+    SSTAMP(t_fw);
     // ---- 4. forward over the segment: rollout, costate, PDAS re-guess ----
     bool changed = false;
     int fi = N;      // single-flip passes: this segment's first flip (stage) ...
@@ -509,20 +540,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
     const bool qchanged = (fold(__ballot(changed)) >> sl) & 1ull;
+    SACC(acc_fw, t_fw);
     if (!qchanged && !done) {
       done = true;
       iters = pass + 1;
     }
   }
 
+  SSTAMP(t_out);
   // ---- output sweep: u* = K x + k from the final gains, x* by the fp64 rollout ----
   const bool solved = done && !bad;
   const float nanv = __int_as_float(0x7fc00000);
   float* uo = uout + (size_t)b * 2 * N;
   float* xo = xout + (size_t)b * 3 * (N + 1);
   if (qowner) {
-    xo[0] = solved ? x0g[3 * b + 0] : nanv;
-    xo[1] = solved ? x0g[3 * b + 1] : nanv;
+    xo[0] = solved ? fX0 : nanv;
+    xo[1] = solved ? fY0 : nanv;
     xo[2] = solved ? fTH0 : nanv;
   }
   const bool want_obj = oo.obj || oo.cost;
@@ -578,20 +611,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (iters_out) iters_out[b] = bad ? 0 : (done ? iters : max_pass);
   }
   if (ws.act) {  // active set of this solution for the next tick (OR over the segments)
-    unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
+    // the lane's 2m bits (input a of stage t at bit 2t + a), placed at bit 2 s0 of the pair
+    unsigned long long lw = 0, hw = 0;
     for (int t = 0; t < m; t++) {
-      const int st = ap[t * 64];
-#pragma unroll
-      for (int a = 0; a < 2; a++) {
-        const int va = 2 * (s0 + t) + a, ca = (st >> (2 * a)) & 3;
-        const unsigned long long bit = 1ull << (va & 63);
-        const unsigned long long in0 = va < 64 ? bit : 0ull, in1 = va < 64 ? 0ull : bit;
-        lo0 |= (ca == 1) ? in0 : 0ull;
-        lo1 |= (ca == 1) ? in1 : 0ull;
-        hi0 |= (ca == 2) ? in0 : 0ull;
-        hi1 |= (ca == 2) ? in1 : 0ull;
-      }
+      const unsigned st = (unsigned)ap[t * 64];
+      const unsigned l2 = (st & 1u) | ((st >> 1) & 2u), h2 = ((st >> 1) & 1u) | ((st >> 2) & 2u);
+      lw |= (unsigned long long)l2 << (2 * t);
+      hw |= (unsigned long long)h2 << (2 * t);
     }
+    const int sh = 2 * s0;
+    unsigned long long lo0 = sh < 64 ? lw << sh : 0ull, hi0 = sh < 64 ? hw << sh : 0ull;
+    unsigned long long lo1 = sh == 0 ? 0ull : (sh < 64 ? lw >> (64 - sh) : lw << (sh - 64));
+    unsigned long long hi1 = sh == 0 ? 0ull : (sh < 64 ? hw >> (64 - sh) : hw << (sh - 64));
 #pragma unroll
     for (int k = L; k < 64; k <<= 1) {
       lo0 |= __shfl_xor(lo0, k, 64);
@@ -612,6 +643,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
     }
   }
+#ifdef F110QP_STAMPS
+  if (lane == 0 && blockIdx.x < 4096) {
+    unsigned long long* o = g_sstamps + (size_t)blockIdx.x * kSegStampSlots;
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    o[0] = t_setup; o[1] = acc_bw; o[2] = acc_dual; o[3] = acc_ref; o[4] = acc_fw;
+    o[5] = t_end - t_out; o[6] = npass; o[7] = t_end - t_start;
+  }
+#endif
 }
 
 template <int S, bool ROT>
@@ -632,3 +671,10 @@ hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const flo
 }
 
 }  // namespace f110qp
+
+#ifdef F110QP_STAMPS
+extern "C" int f110qp_read_seg_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(f110qp::g_sstamps),
+                                  (size_t)n * f110qp::kSegStampSlots * sizeof(unsigned long long));
+}
+#endif

@@ -111,14 +111,14 @@ def test_capi_raises_when_library_missing(monkeypatch):
 
 def test_auto_backend_policy(capi):
     """BACKEND_AUTO: the wave kernel for small box batches and for gap rows, the lane kernel
-    from the measured crossover (3,072 QPs at N <= 32; 768 at N > 32)."""
+    from the measured crossover (1,536 QPs at N <= 32; every batch at N > 32)."""
     assert capi.auto_backend(20, 1024, False) == capi.BACKEND_WAVE
-    assert capi.auto_backend(20, 3071, False) == capi.BACKEND_WAVE
-    assert capi.auto_backend(20, 3072, False) == capi.BACKEND_LANE
+    assert capi.auto_backend(20, 1535, False) == capi.BACKEND_WAVE
+    assert capi.auto_backend(20, 1536, False) == capi.BACKEND_LANE
     assert capi.auto_backend(20, 4096, False) == capi.BACKEND_LANE
     assert capi.auto_backend(20, 65536, True) == capi.BACKEND_WAVE
-    assert capi.auto_backend(40, 768, False) == capi.BACKEND_LANE
-    assert capi.auto_backend(40, 767, False) == capi.BACKEND_WAVE
+    assert capi.auto_backend(40, 1, False) == capi.BACKEND_LANE
+    assert capi.auto_backend(40, 768, True) == capi.BACKEND_WAVE
 
 
 def test_auto_backend_grouped_policy(capi):
@@ -126,8 +126,8 @@ def test_auto_backend_grouped_policy(capi):
     C4 batch run on the lane kernel (grouped wave measured 1,041 vs 240 us at the shard)."""
     assert capi.auto_backend(40, 8192, False, grouped=True) == capi.BACKEND_LANE
     assert capi.auto_backend(40, 65536, False, grouped=True) == capi.BACKEND_LANE
-    assert capi.auto_backend(40, 767, False, grouped=True) == capi.BACKEND_WAVE
-    assert capi.auto_backend(20, 3071, False, grouped=True) == capi.BACKEND_WAVE
+    assert capi.auto_backend(40, 1, False, grouped=True) == capi.BACKEND_LANE
+    assert capi.auto_backend(20, 1535, False, grouped=True) == capi.BACKEND_WAVE
 
 
 def test_qp_dims_match_reference_sizes(capi, oracle):
@@ -148,7 +148,7 @@ def test_backend_info_resolves_auto_and_scratch(capi):
     assert s20.backend_info(4096) == (capi.BACKEND_LANE, 16, 1)
     assert s20.backend_info(65536) == (capi.BACKEND_LANE, 64, 4)
     s40 = capi.Solver(capi.default_config(40))
-    assert s40.backend_info(capi.LANE_MIN_BATCH_WIDE - 1)[0] == capi.BACKEND_WAVE
+    assert s40.backend_info(1)[0] == capi.BACKEND_LANE
     # small batches split every QP's horizon over S lanes (lane_seg_kernel.h): 64 / S QPs per wave
     assert s40.backend_info(8192, grouped=True) == (capi.BACKEND_LANE, 8, 1)
     assert s40.lane_segments(8192) == 8 and s20.lane_segments(4096) == 4
