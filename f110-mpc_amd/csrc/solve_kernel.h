@@ -827,6 +827,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     const double pxa = a ? 0.0 : M.b00, pya = a ? 0.0 : M.b10;  // dk = 0 in this regime
     const double sxa = M.a02 * beta_a, sya = M.a12 * beta_a;
     double C0[R][2], C1[R][2];
+    bool stiff = false;
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const double T = (double)(N - kk[r]);
@@ -842,28 +843,74 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         C0[r][bb] = q0 * (ax_b * Ux + sxb * Vx) + q1 * (ay_b * Uy + syb * Vy) + q2 * T * beta_a * beta_b;
         C1[r][bb] = q0 * sxb * Ux + q1 * syb * Uy;
       }
-      if (vv[r] < NUM) {
+      // a row cancels in fp32 when |C1| (k - l) reaches its diagonal's magnitude
+      const double dg = (a ? C0[r][1] : C0[r][0]) + ra;
+      stiff |= valid[r] && (fabs(C1[r][0]) + fabs(C1[r][1])) * (double)N > 4.0 * fabs(dg);
+    }
+    // fp32 entries for box-only QPs of one register row (N <= 32) when no row cancels (the
+    // shipped dt = 0.01: |C1| N is a few percent of the diagonal; the round-2 formation), fp64
+    // entries rounded once otherwise (wave-uniform). The gap kernel always takes fp64: GI's
+    // final fp64 check at N = 40 rejected a point built on fp32 entries (test_horizons_gap[40]).
+    if (!GAP && R == 1 && __ballot(stiff) == 0ull) {
+      float C0f[R][2], C1f[R][2];
+#pragma unroll
+      for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int bb = 0; bb < 2; bb++) {
+          C0f[r][bb] = (float)C0[r][bb];
+          C1f[r][bb] = (float)C1[r][bb];
+        }
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (vv[r] < NUM) {
+#pragma unroll
+          for (int w = 0; w < NUM; w++) {
+            const int l = w >> 1, bb = w & 1;
+            sm.L[vv[r]][w] = fmaf(C1f[r][bb], (float)(kk[r] - l), C0f[r][bb]);
+          }
+        }
+      }
+      wsync();
+#pragma unroll
+      for (int r = 0; r < R; r++) {
 #pragma unroll
         for (int w = 0; w < NUM; w++) {
-          const int l = w >> 1, bb = w & 1;  // exchange via L: row stride NUM + 1, conflict-free
-          sm.L[vv[r]][w] = (float)fma(C1[r][bb], (double)(kk[r] - l), C0[r][bb]);
+          const int l = w >> 1, bb = w & 1;
+          float h;
+          if (w == vv[r]) h = (float)(C0[r][bb] + ra);
+          else h = (l <= kk[r]) ? fmaf(C1f[r][bb], (float)(kk[r] - l), C0f[r][bb]) : sm.L[w][cl[r]];
+          const bool ok = valid[r] && (w < NU);
+          hrow[r][w] = ok ? h : (w == vv[r] ? 1.f : 0.f);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (vv[r] < NUM) {
+#pragma unroll
+          for (int w = 0; w < NUM; w++) {
+            const int l = w >> 1, bb = w & 1;  // exchange via L: row stride NUM + 1, conflict-free
+            sm.L[vv[r]][w] = (float)fma(C1[r][bb], (double)(kk[r] - l), C0[r][bb]);
+          }
+        }
+      }
+      wsync();
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+#pragma unroll
+        for (int w = 0; w < NUM; w++) {
+          const int l = w >> 1, bb = w & 1;
+          float h;
+          if (w == vv[r]) h = (float)(C0[r][bb] + ra);
+          else h = (l <= kk[r]) ? (float)fma(C1[r][bb], (double)(kk[r] - l), C0[r][bb]) : sm.L[w][cl[r]];
+          const bool ok = valid[r] && (w < NU);
+          hrow[r][w] = ok ? h : (w == vv[r] ? 1.f : 0.f);
         }
       }
     }
-    wsync();
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-#pragma unroll
-      for (int w = 0; w < NUM; w++) {
-        const int l = w >> 1, bb = w & 1;
-        float h;
-        if (w == vv[r]) h = (float)(C0[r][bb] + ra);
-        else h = (l <= kk[r]) ? (float)fma(C1[r][bb], (double)(kk[r] - l), C0[r][bb]) : sm.L[w][cl[r]];
-        const bool ok = valid[r] && (w < NU);
-        hrow[r][w] = ok ? h : (w == vv[r] ? 1.f : 0.f);
-      }
+    for (int r = 0; r < R; r++)
       hd[r] = vv[r] < NUM ? (valid[r] ? (float)((a ? C0[r][1] : C0[r][0]) + ra) : 1.f) : 0.f;
-    }
     wsync();
   };
   if (whit) {
