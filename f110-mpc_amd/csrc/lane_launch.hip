@@ -15,19 +15,20 @@ template <int S, bool ROT>
 hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                              float* uo, float* xo, int* st, int* its, const WarmState& ws,
                              const LaneWork& lw, const ObjOut& oo, hipStream_t s);  // lane_seg_inst.hip
-constexpr size_t seg_lds_per_wave(int N, int S) { return (size_t)(N / S) * 64 * (3 * 8 + 4 + 11 * 8); }
+constexpr size_t seg_lds_per_wave(int N, int S) { return (size_t)((N + S - 1) / S) * 64 * (3 * 8 + 4 + 11 * 8); }
 
 // Horizon segments per QP (lane_seg_kernel.h). A batch whose waves leave SIMDs idle (the QPs fit
 // in fewer than one wave per SIMD at 64 / S QPs per wave) splits every QP's horizon over S lanes
-// instead of running 64 / L identical copies of it. S divides N into segments of >= 2 stages, the
-// grid stays within one wave per SIMD (1,024 waves) and the segmented LDS fits. Among those the
-// launch takes the S with the shortest per-pass chain by the instruction model of DESIGN.md 2b:
-// sequential N x ~255 instructions, segmented (N / S) x ~350 + (S - 1) x ~230 (the two segment
-// recursions). A forced QPs-per-wave or scratch placement keeps lane_kernel.h.
+// instead of running 64 / L identical copies of it. S cuts N into segments of >= 2 stages (of
+// floor(N / S) or one more), the grid stays within one wave per SIMD (1,024 waves) and the
+// segmented LDS fits. Among those the launch takes the S with the shortest per-pass chain by the
+// instruction model of DESIGN.md 2b': sequential N x ~255 instructions, segmented ceil(N / S) x
+// ~350 + (S - 1) x ~230 (the two segment recursions). A forced QPs-per-wave or scratch placement
+// keeps lane_kernel.h.
 int lane_segments(const KParams& P, int B, const LaneWork& lw) {
   const int N = P.N;
   auto fits = [&](int S) {
-    if (N % S != 0 || N / S < 2) return false;
+    if (N / S < 2) return false;
     const size_t waves = ((size_t)B * S + 63) / 64;
     const size_t per_cu = (waves + 255) / 256;
     return per_cu <= 4 && per_cu * seg_lds_per_wave(N, S) <= 160 * 1024;
@@ -39,7 +40,7 @@ int lane_segments(const KParams& P, int B, const LaneWork& lw) {
   double cbest = 255.0 * N;
   for (int S = 2; S <= 8; S <<= 1) {
     if (!fits(S)) continue;
-    const double c = 350.0 * (N / S) + 230.0 * (S - 1);
+    const double c = 350.0 * ((N + S - 1) / S) + 230.0 * (S - 1);
     if (c < cbest) {
       best = S;
       cbest = c;

@@ -59,8 +59,9 @@ __device__ unsigned long long g_sstamps[4096 * kSegStampSlots];
 #define SACC(acc, since)
 #endif
 
-// LDS bytes per wave of the segmented kernel for horizon N split into S segments
-constexpr size_t seg_lds_bytes(int N, int S) { return (size_t)(N / S) * 64 * (3 * 8 + 4 + 11 * 8); }
+// LDS bytes per wave of the segmented kernel for horizon N split into S segments (rows for the
+// longest segment, ceil(N / S) stages)
+constexpr size_t seg_lds_bytes(int N, int S) { return (size_t)((N + S - 1) / S) * 64 * (3 * 8 + 4 + 11 * 8); }
 
 template <int S>
 __device__ __forceinline__ double seg_shfl(double v, int src) {
@@ -85,8 +86,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const bool qowner = owner && seg == 0;
   const int b = b0 + slot;
   const int N = P.N;
-  const int m = N / S;
-  const int s0 = seg * m;
+  // segments of q or q + 1 stages (the first N mod S ones longer); LDS rows for the longest
+  const int q = N / S, rem = N - q * S;
+  const int m = q + (seg < rem ? 1 : 0);
+  const int s0 = seg * q + (seg < rem ? seg : rem);
+  const int mM = q + (rem > 0 ? 1 : 0);
   const bool top = seg == S - 1;
   const int up = (lane + L) & 63, dn = (lane - L) & 63;  // same QP, segment + 1 / - 1 (ring)
 
@@ -94,9 +98,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #ifdef F110QP_STAMPS
   unsigned long long acc_bw = 0, acc_dual = 0, acc_ref = 0, acc_fw = 0, t_setup = 0, npass = 0;
 #endif
-  double* const r64 = seg_smem + lane;                                   // [3m][64]
-  int* const ap = reinterpret_cast<int*>(seg_smem + 3 * m * 64) + lane;  // [m][64]
-  double* const sc = seg_smem + 3 * m * 64 + m * 32 + lane;              // [m][11][64]
+  double* const r64 = seg_smem + lane;                                     // [3mM][64]
+  int* const ap = reinterpret_cast<int*>(seg_smem + 3 * mM * 64) + lane;  // [mM][64]
+  double* const sc = seg_smem + 3 * mM * 64 + mM * 32 + lane;             // [mM][11][64]
 
   // per-QP inputs and the warm-start key, issued before the staging loads so that both share
   // one HBM round trip
@@ -113,7 +117,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // valid address (clamped) and every store lands (past the staged rows for e >= tot), so the
   // loop has no EXEC-masked region: ~11 instructions per element instead of ~50 (ISA).
   {
-    float* stg = reinterpret_cast<float*>(seg_smem + 3 * m * 64 + m * 32);
+    float* stg = reinterpret_cast<float*>(seg_smem + 3 * mM * 64 + mM * 32);
     const int n3 = 3 * N, S3 = 3 * P.xr_stride, tot = nq * n3;
     const float* src = xrg + (size_t)b0 * S3;
     const int dq = 64 / n3, dc = 64 - dq * n3;
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   // entry flags the QP (one ballot folded over its segment lanes)
   bool nonfin = false;
   {
-    const float* stg = reinterpret_cast<const float*>(seg_smem + 3 * m * 64 + m * 32);
+    const float* stg = reinterpret_cast<const float*>(seg_smem + 3 * mM * 64 + mM * 32);
     for (int t = 0; t < m; t++) {
       const int i = s0 + t;
       const float fx = stg[(3 * i + 0) * L + slot], fy = stg[(3 * i + 1) * L + slot];

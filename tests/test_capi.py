@@ -153,6 +153,12 @@ def test_backend_info_resolves_auto_and_scratch(capi):
     assert s40.backend_info(8192, grouped=True) == (capi.BACKEND_LANE, 8, 1)
     assert s40.lane_segments(8192) == 8 and s20.lane_segments(4096) == 4
     assert s20.lane_segments(65536) == 1 and s20.lane_segments(1024) == 1  # 1,024: wave back end
+    # horizons S does not divide: segments of floor(N / S) or one more stage (the reference's
+    # default N = 30 and odd N)
+    s30, s25 = capi.Solver(capi.default_config(30)), capi.Solver(capi.default_config(25))
+    assert s30.lane_segments(4096) == 8 and s25.lane_segments(4096) == 8 and s30.lane_segments(16384) == 1  # S = 2 would need 222 KB of LDS per CU
+    s30.close()
+    s25.close()
     assert s40.backend_info(65536, grouped=True) == (capi.BACKEND_LANE, 64, 4)
     sg = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE))
     assert sg.backend_info(65536)[0] == capi.BACKEND_WAVE

@@ -16,10 +16,12 @@ def _lane(capi, N, **cfg):
     return capi.Solver(capi.default_config(N, backend=capi.BACKEND_LANE, **cfg))
 
 
-@pytest.mark.parametrize("S,N", [(2, 2), (2, 10), (4, 20), (2, 30), (8, 40), (4, 40), (2, 40), (8, 48), (4, 4), (8, 16)])
+@pytest.mark.parametrize("S,N", [(2, 2), (2, 10), (4, 20), (2, 30), (8, 40), (4, 40), (2, 40), (8, 48), (4, 4),
+                                 (8, 16), (4, 30), (8, 30), (8, 20), (4, 17), (2, 25), (8, 47), (4, 9), (2, 3)])
 def test_segments_horizons(oracle, capi, monkeypatch, S, N):
-    """Every segment count on horizons it divides (segments of 1.. 24 stages), many active bounds
-    on both faces, batch not a multiple of the QPs per wave."""
+    """Every segment count on horizons it divides and on horizons it does not (segments of
+    floor(N / S) or one more stage, 2 .. 24), many active bounds on both faces, batch not a
+    multiple of the QPs per wave; N / S < 2 keeps the sequential kernel."""
     monkeypatch.setenv("F110QP_LANE_SEG", str(S))
     w = workload.make_batch(1000, N, seed=9100 + 10 * S + N, heading="true", lateral=1.5, steer_range=1.0)
     s = _lane(capi, N)
