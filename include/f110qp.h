@@ -157,7 +157,8 @@ int f110qp_solve_batch_dev(f110qp_ctx* ctx, int batch, const float* x0, const fl
  * equal that member's reuses it, any other QP (or an id outside [0, num_groups)) builds its own.
  * Grouping therefore never changes a result: the output is bit-identical to
  * f110qp_solve_batch[_dev] on the wave back end. The lane back end (chosen by AUTO at and above
- * F110QP_LANE_MIN_BATCH_GROUPED[_WIDE]) has no factor to share and ignores the groups. Grouped
+ * F110QP_LANE_MIN_BATCH_GROUPED[_WIDE]) ignores the groups (only its first, cold pass has
+ * group-invariant Riccati matrices: <= ~4% of a C4 launch). Grouped
  * calls neither use nor update the warm-start state. Same layouts and conventions as above. */
 int f110qp_solve_grouped(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
                          const float* x_ref, const float* halfspace, const int* group,
