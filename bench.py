@@ -298,7 +298,7 @@ def main():
                     help="grouped solve (one W = H^-1 per 120-candidate scenario, f110qp_solve_grouped_dev); "
                          "auto = on for c4")
     ap.add_argument("--backend", default="auto", choices=["auto", "wave", "lane"],
-                    help="solver back end (auto: lane-per-QP for box-only batches >= capi.LANE_MIN_BATCH = 1536 "
+                    help="solver back end (auto: lane-per-QP for box-only batches >= capi.LANE_MIN_BATCH = 1024 "
                          "at N <= 32, >= capi.LANE_MIN_BATCH_WIDE = 1 at N > 32; f110qp_backend_info)")
     args = ap.parse_args()
 

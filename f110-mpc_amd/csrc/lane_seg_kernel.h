@@ -63,13 +63,24 @@ __device__ unsigned long long g_sstamps[4096 * kSegStampSlots];
 // longest segment, ceil(N / S) stages)
 constexpr size_t seg_lds_bytes(int N, int S) { return (size_t)((N + S - 1) / S) * 64 * (3 * 8 + 4 + 11 * 8); }
 
+template <int M>
+struct SegMode {
+  static constexpr int value = M;
+};
+
 template <int S>
 __device__ __forceinline__ double seg_shfl(double v, int src) {
   return __shfl(v, src, 64);
 }
 
+#ifndef F110QP_SEG_WPE
+// waves-per-EU hint: 2 (<= 256 VGPRs; the grid still runs one wave per SIMD or CU) schedules
+// better than 1: same-box A/B C5 31.2 -> 30.6 us, C2 on the lane back end 28.3 -> 27.7, C4 shard
+// neutral (tools/ab_seg_variant.sh)
+#define F110QP_SEG_WPE 2
+#endif
 template <int S, bool ROT>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void lane_seg_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_WPE, F110QP_SEG_WPE))) void lane_seg_kernel(
     const KParams P, const int B, const float* __restrict__ x0g, const float* __restrict__ ulg,
     const float* __restrict__ xrg, float* __restrict__ uout, float* __restrict__ xout,
     int* __restrict__ status_out, int* __restrict__ iters_out, const WarmState ws, const int kmax,
@@ -200,7 +211,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const unsigned kth = __float_as_uint(fTH0), kv = __float_as_uint(fv), kd = __float_as_uint(fd);
   {
     unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
+#ifdef F110QP_SEG_SEED_ANY  // measurement knob: seed from the slot's previous set on any key
+                            // (measured C5 31.2 -> 34.9 us: the stale set costs passes)
+    const bool hit = ws.act && ws.key && key3 != 0u;
+#else
     const bool hit = ws.act && ws.key && key3 != 0u && key0 == kth && key1 == kv && key2 == kd;
+#endif
     if (hit) {
       lo0 = ws.act[2 * R * b];
       hi0 = ws.act[2 * R * b + 1];
@@ -467,10 +483,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     SACC(acc_ref, t_ref);
     SSTAMP(t_fw);
     // ---- 4. forward over the segment: rollout, costate, PDAS re-guess ----
+    // Two instantiations as in lane_kernel.h: plain PDAS passes (MODE 0) store the re-guessed
+    // state as it is; single-flip passes (MODE 1) take the segment's first change only and
+    // remember it (stage, replaced state) for the min over the QP's lanes below.
     bool changed = false;
-    int fi = N;      // single-flip passes: this segment's first flip (stage) ...
+    int fi = N;       // single-flip passes: this segment's first flip (stage) ...
     int fold_st = 0;  // ... and the state it replaced
-    {
+    auto forward = [&](auto mode_tag) {
+      constexpr int MODE = decltype(mode_tag)::value;
       double x0 = xs0, x1 = xs1, x2 = xs2;
       double l0 = P00 * x0 + P01 * x1 + P02 * x2 + p0 + pl0;  // costate at x_s
       double l1 = P01 * x0 + P11 * x1 + P12 * x2 + p1 + pl1;
@@ -506,7 +526,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         const double g0 = ROT ? r0 * (u0 - ud0) + b00 * l0 + b20 * l2
                               : r0 * (u0 - ud0) + b00 * l0 + b10 * l1 + b20 * l2;
         const double g1 = r1 * (u1 - ud1) + b21 * l2;
-        int st = old;
+        int st = MODE ? old : 0;
 #pragma unroll
         for (int a = 0; a < 2; a++) {
           const int ca = (old >> (2 * a)) & 3;
@@ -515,13 +535,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           const bool nlo = ((ca == 1) & (g > -gta)) | ((ca == 0) & (u < (a ? lbe1 : lbe0)));
           const bool nhi = !nlo & (((ca == 2) & (g < gta)) | ((ca == 0) & (u > (a ? ube1 : ube0))));
           const int nca = (int)nlo | ((int)nhi << 1);
-          const bool take = (nca != ca) & !(single & flipped);
-          st = take ? ((st & ~(3 << (2 * a))) | (nca << (2 * a))) : st;
-          flipped |= take;
+          if constexpr (MODE == 0) {
+            st |= nca << (2 * a);
+          } else {
+            const bool take = (nca != ca) & !flipped;
+            st = take ? ((st & ~(3 << (2 * a))) | (nca << (2 * a))) : st;
+            flipped |= take;
+          }
         }
         const bool ch = st != old;
-        fi = (ch & (fi == N)) ? s0 + t : fi;
-        fold_st = (ch & (fi == s0 + t)) ? old : fold_st;
+        if constexpr (MODE == 1) {
+          fi = (ch & (fi == N)) ? s0 + t : fi;
+          fold_st = (ch & (fi == s0 + t)) ? old : fold_st;
+        }
         changed |= ch;
         ap[t * 64] = st;
         const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
@@ -529,7 +555,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
         x0 = nx0; x1 = nx1; x2 = nx2;
       }
-    }
+    };
+    if (single) forward(SegMode<1>{});
+    else forward(SegMode<0>{});
     // single-flip passes keep only the QP's first flip over the whole horizon
     if (single) {
       int mn = fi;

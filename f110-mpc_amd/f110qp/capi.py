@@ -29,7 +29,7 @@ GAP_ACTIVE = 1
 BACKEND_AUTO = 0
 BACKEND_WAVE = 1
 BACKEND_LANE = 2
-LANE_MIN_BATCH = 1536
+LANE_MIN_BATCH = 1024
 LANE_MIN_BATCH_WIDE = 1
 LANE_MIN_BATCH_GROUPED = LANE_MIN_BATCH
 LANE_MIN_BATCH_GROUPED_WIDE = LANE_MIN_BATCH_WIDE

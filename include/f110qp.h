@@ -84,13 +84,14 @@ extern "C" {
                                   /* gap rows always use the wave back end)                    */
 /* AUTO thresholds, measured on MI355X (kernel us, DESIGN.md section 6, round 3: the lane back end
  * with the partitioned-horizon kernel below one wave per SIMD, the wave back end with its fp64
- * certification). N = 20 (C2 recipe, cold): wave 27.3 vs lane 30.6 at 512, 29.9 vs 30.7 at 1,024,
- * 53.1 vs 36.3 at 2,048, 93.0 vs 37.0 at 3,072. N = 30: 94.8 vs 77.9 at 2,048. N = 40: wave 223
- * vs lane 45.7 at 256, 365 vs 46.1 at 512, 428 vs 53.7 at 768: the lane back end from one QP on.
+ * certification). N = 20 (C2 recipe, cold): wave 27.3 vs lane 30.6 at 512 (before the last
+ * segmented-kernel changes), 28.5 vs 27.7 at 1,024, 53.1 vs 36.3 at 2,048, 93.0 vs 37.0 at
+ * 3,072. N = 30: 94.8 vs 77.9 at 2,048. N = 40: wave 223 vs lane 45.7 at 256, 365 vs 46.1 at
+ * 512, 428 vs 53.7 at 768: the lane back end from one QP on.
  * Grouped calls use the same thresholds: the wave back end's per-group W saves its inverse but
  * its per-QP active-set phase still dominates (C4 candidate sets: 8,192 x N=40 grouped wave
  * 1,041 us vs lane 240 us, round 2). */
-#define F110QP_LANE_MIN_BATCH 1536
+#define F110QP_LANE_MIN_BATCH 1024
 #define F110QP_LANE_MIN_BATCH_WIDE 1
 #define F110QP_LANE_MIN_BATCH_GROUPED F110QP_LANE_MIN_BATCH
 #define F110QP_LANE_MIN_BATCH_GROUPED_WIDE F110QP_LANE_MIN_BATCH_WIDE

@@ -111,10 +111,10 @@ def test_capi_raises_when_library_missing(monkeypatch):
 
 def test_auto_backend_policy(capi):
     """BACKEND_AUTO: the wave kernel for small box batches and for gap rows, the lane kernel
-    from the measured crossover (1,536 QPs at N <= 32; every batch at N > 32)."""
-    assert capi.auto_backend(20, 1024, False) == capi.BACKEND_WAVE
-    assert capi.auto_backend(20, 1535, False) == capi.BACKEND_WAVE
-    assert capi.auto_backend(20, 1536, False) == capi.BACKEND_LANE
+    from the measured crossover (1,024 QPs at N <= 32; every batch at N > 32)."""
+    assert capi.auto_backend(20, 512, False) == capi.BACKEND_WAVE
+    assert capi.auto_backend(20, 1023, False) == capi.BACKEND_WAVE
+    assert capi.auto_backend(20, 1024, False) == capi.BACKEND_LANE
     assert capi.auto_backend(20, 4096, False) == capi.BACKEND_LANE
     assert capi.auto_backend(20, 65536, True) == capi.BACKEND_WAVE
     assert capi.auto_backend(40, 1, False) == capi.BACKEND_LANE
@@ -127,7 +127,7 @@ def test_auto_backend_grouped_policy(capi):
     assert capi.auto_backend(40, 8192, False, grouped=True) == capi.BACKEND_LANE
     assert capi.auto_backend(40, 65536, False, grouped=True) == capi.BACKEND_LANE
     assert capi.auto_backend(40, 1, False, grouped=True) == capi.BACKEND_LANE
-    assert capi.auto_backend(20, 1535, False, grouped=True) == capi.BACKEND_WAVE
+    assert capi.auto_backend(20, 1023, False, grouped=True) == capi.BACKEND_WAVE
 
 
 def test_qp_dims_match_reference_sizes(capi, oracle):
@@ -143,7 +143,8 @@ def test_backend_info_resolves_auto_and_scratch(capi):
     the lane QPs-per-wave fill <= 256 waves; the scratch sits in LDS (fp64 when it fits) while the
     grid's waves are resident with it and in HBM (fp32) at the C4 size."""
     s20 = capi.Solver(capi.default_config(20))
-    assert s20.backend_info(1024) == (capi.BACKEND_WAVE, 1, 0)
+    assert s20.backend_info(512) == (capi.BACKEND_WAVE, 1, 0)
+    assert s20.backend_info(1024) == (capi.BACKEND_LANE, 16, 1)  # C2: segmented, S = 4
     assert s20.backend_info(capi.LANE_MIN_BATCH)[0] == capi.BACKEND_LANE
     assert s20.backend_info(4096) == (capi.BACKEND_LANE, 16, 1)
     assert s20.backend_info(65536) == (capi.BACKEND_LANE, 64, 4)
@@ -152,7 +153,7 @@ def test_backend_info_resolves_auto_and_scratch(capi):
     # small batches split every QP's horizon over S lanes (lane_seg_kernel.h): 64 / S QPs per wave
     assert s40.backend_info(8192, grouped=True) == (capi.BACKEND_LANE, 8, 1)
     assert s40.lane_segments(8192) == 8 and s20.lane_segments(4096) == 4
-    assert s20.lane_segments(65536) == 1 and s20.lane_segments(1024) == 1  # 1,024: wave back end
+    assert s20.lane_segments(65536) == 1 and s20.lane_segments(1024) == 4 and s20.lane_segments(512) == 1
     # horizons S does not divide: segments of floor(N / S) or one more stage (the reference's
     # default N = 30 and odd N)
     s30, s25 = capi.Solver(capi.default_config(30)), capi.Solver(capi.default_config(25))
