@@ -1,3 +1,5 @@
+# Same-box A/B of the wave kernel against a variant library (F110QP_LIB): -m gpu on the in-tree
+# library, then C2 / C3 / tick kernel times from both. Usage on the GPU box: bash tools/ab_solve_variant.sh
 mkdir -p gpurun_out/ab1
 V=f110-mpc_amd/lib_var/base/libf110qp.so
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/ab1/gpu_tests_var.log 2>&1 || { tail -30 gpurun_out/ab1/gpu_tests_var.log; exit 3; }

@@ -1,3 +1,5 @@
+# Wave vs lane back-end crossover sweep behind the AUTO thresholds (include/f110qp.h), plus the -m gpu
+# suite first; lines under profiles/r03/seg/crossover.txt. Usage on the GPU box: bash tools/crossover.sh
 mkdir -p gpurun_out/v3
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/v3/gpu_tests.log 2>&1 || { tail -30 gpurun_out/v3/gpu_tests.log; exit 3; }
 tail -1 gpurun_out/v3/gpu_tests.log
