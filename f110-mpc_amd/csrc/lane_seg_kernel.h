@@ -50,7 +50,7 @@ namespace f110qp {
 // Diagnostic build only (-DF110QP_STAMPS on lane_seg_inst.hip): per-wave cycles of the setup, each
 // pass phase and the output, read back with f110qp_read_seg_stamps(). Never in the shipped library.
 #ifdef F110QP_STAMPS
-constexpr int kSegStampSlots = 8;
+constexpr int kSegStampSlots = 12;
 __device__ unsigned long long g_sstamps[4096 * kSegStampSlots];
 #define SSTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #define SACC(acc, since) acc += __builtin_amdgcn_s_memtime() - (since)
@@ -156,6 +156,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     __syncthreads();
   }
 
+  SSTAMP(t_stg);
   // ---- per-lane QP data (Model::Linearize, model.cpp:30-59), as lane_kernel.h ----
   const double X0 = (double)fX0, Y0 = (double)fY0;
   const double th0 = (double)fTH0;
@@ -184,6 +185,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   const double gtol0 = gt * (1.0 + r0 * (1.0 + fabs(lb0) + fabs(ub0)));
   const double gtol1 = gt * (1.0 + r1 * (1.0 + fabs(lb1) + fabs(ub1)));
 
+  SSTAMP(t_lin);
   // references of the lane's stages: recentred (ROT: rotated) fp64, lane-major; a non-finite
   // entry flags the QP (one ballot folded over its segment lanes)
   bool nonfin = false;
@@ -201,6 +203,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     }
     __syncthreads();  // the staging region becomes the Riccati scratch
   }
+  SSTAMP(t_conv);
   // terminal reference x_ref[N-1] (mpc.cpp:228): the last stage of the top segment
   const double rNx = __shfl(r64[(3 * (m - 1) + 0) * 64], (lane | (63 & ~(L - 1))) & 63);
   const double rNy = __shfl(r64[(3 * (m - 1) + 1) * 64], (lane | (63 & ~(L - 1))) & 63);
@@ -681,6 +684,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     const unsigned long long t_end = __builtin_amdgcn_s_memtime();
     o[0] = t_setup; o[1] = acc_bw; o[2] = acc_dual; o[3] = acc_ref; o[4] = acc_fw;
     o[5] = t_end - t_out; o[6] = npass; o[7] = t_end - t_start;
+    o[8] = t_stg - t_start; o[9] = t_lin - t_stg; o[10] = t_conv - t_lin; o[11] = t_setup - (t_conv - t_start);
   }
 #endif
 }
