@@ -61,7 +61,10 @@ __device__ unsigned long long g_sstamps[4096 * kSegStampSlots];
 
 // LDS bytes per wave of the segmented kernel for horizon N split into S segments (rows for the
 // longest segment, ceil(N / S) stages)
-constexpr size_t seg_lds_bytes(int N, int S) { return (size_t)((N + S - 1) / S) * 64 * (3 * 8 + 4 + 11 * 8); }
+// FST: the scratch keeps the lam-gains F_i (6) instead of S_i^-1 (3): 14 doubles per stage
+constexpr size_t seg_lds_bytes(int N, int S, bool fst = false) {
+  return (size_t)((N + S - 1) / S) * 64 * (3 * 8 + 4 + (fst ? 14 : 11) * 8);
+}
 
 template <int M>
 struct SegMode {
@@ -79,13 +82,14 @@ __device__ __forceinline__ double seg_shfl(double v, int src) {
 // neutral (tools/ab_seg_variant.sh)
 #define F110QP_SEG_WPE 2
 #endif
-template <int S, bool ROT>
+template <int S, bool ROT, bool FST>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_WPE, F110QP_SEG_WPE))) void lane_seg_kernel(
     const KParams P, const int B, const float* __restrict__ x0g, const float* __restrict__ ulg,
     const float* __restrict__ xrg, float* __restrict__ uout, float* __restrict__ xout,
     int* __restrict__ status_out, int* __restrict__ iters_out, const WarmState ws, const int kmax,
     const ObjOut oo) {
   constexpr int L = 64 / S;  // QPs per wave
+  constexpr int NV = FST ? 14 : 11;  // scratch doubles per stage: K 6, k 2, then F 6 or S^-1 3
   extern __shared__ __attribute__((aligned(16))) double seg_smem[];
   const int lane = threadIdx.x;
   const int sl = lane & (L - 1);
@@ -111,7 +115,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
 #endif
   double* const r64 = seg_smem + lane;                                     // [3mM][64]
   int* const ap = reinterpret_cast<int*>(seg_smem + 3 * mM * 64) + lane;  // [mM][64]
-  double* const sc = seg_smem + 3 * mM * 64 + mM * 32 + lane;             // [mM][11][64]
+  double* const sc = seg_smem + 3 * mM * 64 + mM * 32 + lane;             // [mM][NV][64]
 
   // per-QP inputs and the warm-start key, issued before the staging loads so that both share
   // one HBM round trip
@@ -250,8 +254,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
                    ((fold(__ballot(nonfin)) >> sl) & 1ull);
   bool done = bad;
   int iters = 0;
-  // the segment's start state of the current pass (kept for the output sweep)
-  double xs0 = 0.0, xs1 = 0.0, xs2 = 0.0;
+  // the segment's start state and terminal multiplier lam_j of the current pass (kept for the
+  // output sweep)
+  double xs0 = 0.0, xs1 = 0.0, xs2 = 0.0, lm0 = 0.0, lm1 = 0.0, lm2 = 0.0;
 
 
   const int max_pass = P.max_iter > kmax ? P.max_iter : kmax;
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       double rx = r64[(3 * (m - 1) + 0) * 64], ry = r64[(3 * (m - 1) + 1) * 64];
       double rt = r64[(3 * (m - 1) + 2) * 64];
       for (int t = m - 1; t >= 0; t--) {
-        double* s = sc + t * 11 * 64;
+        double* s = sc + t * NV * 64;
         const int sti = nst;
         const int tn = t > 0 ? t - 1 : 0;
         nst = ap[tn * 64];
@@ -329,7 +334,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         const double k0 = bA0 - (I00 * w0 + I01 * w1), k1 = bA1 - (I01 * w0 + I11 * w1);
         s[0] = K00; s[64] = K01; s[2 * 64] = K02; s[3 * 64] = K10; s[4 * 64] = K11;
         s[5 * 64] = K12; s[6 * 64] = k0; s[7 * 64] = k1;
-        s[8 * 64] = I00; s[9 * 64] = I01; s[10 * 64] = I11;
+        if constexpr (!FST) {
+          s[8 * 64] = I00; s[9 * 64] = I01; s[10 * 64] = I11;
+        }
         P00 = Y00 + X00 * K00 + X10 * K10;
         P01 = Y01 + X00 * K01 + X10 * K11;
         P02 = Y02 + X00 * K02 + X10 * K12;
@@ -349,6 +356,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         const double L02 = -(I00 * W20 + I01 * W21);
         const double L10 = -(I01 * W00 + I11 * W01), L11 = -(I01 * W10 + I11 * W11);
         const double L12 = -(I01 * W20 + I11 * W21);
+        if constexpr (FST) {
+          s[8 * 64] = L00; s[9 * 64] = L01; s[10 * 64] = L02;
+          s[11 * 64] = L10; s[12 * 64] = L11; s[13 * 64] = L12;
+        }
         // psi += W k + Phi C
         s0v += W00 * k0 + W01 * k1 + (ROT ? F02 * c2 : F00 * c0 + F01 * c1 + F02 * c2);
         s1v += W10 * k0 + W11 * k1 + (ROT ? F12 * c2 : F10 * c0 + F11 * c1 + F12 * c2);
@@ -379,7 +390,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       s0v = s1v = s2v = 0.0;
       G00 = G01 = G02 = G11 = G12 = G22 = 0.0;
     }
-    double lm0 = 0.0, lm1 = 0.0, lm2 = 0.0;  // lam_j
+    lm0 = lm1 = lm2 = 0.0;
     xs0 = xs1 = xs2 = 0.0;
     if constexpr (S > 1) {
       double M00 = P00, M01 = P01, M02 = P02, M11 = P11, M12 = P12, M22 = P22;
@@ -458,19 +469,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     SACC(acc_dual, t_dual);
     SSTAMP(t_ref);
     // ---- 3. refresh: the lam-part of the feed-forward, backward over the segment ----
+    // (FST: nothing to refresh; the forward sweep adds F_i lam_j to k_i and the costate at the
+    // segment start takes p^lam_s = Phi_s' lam_j. Phi's top-lane zeroing is harmless: lam = 0 there.)
     double pl0 = lm0, pl1 = lm1, pl2 = lm2;
-    if constexpr (S > 1) {
+    if constexpr (FST) {
+      pl0 = F00 * lm0 + F10 * lm1 + F20 * lm2;
+      pl1 = F01 * lm0 + F11 * lm1 + F21 * lm2;
+      pl2 = F02 * lm0 + F12 * lm1 + F22 * lm2;
+    }
+    if constexpr (S > 1 && !FST) {
       // stage t - 1's values are loaded while stage t computes (clamped: no branch)
       double nr[11];
 #pragma unroll
-      for (int e = 0; e < 11; e++) nr[e] = sc[((m - 1) * 11 + e) * 64];
+      for (int e = 0; e < 11; e++) nr[e] = sc[((m - 1) * NV + e) * 64];
       for (int t = m - 1; t >= 0; t--) {
-        double* s = sc + t * 11 * 64;
+        double* s = sc + t * NV * 64;
         const double K00 = nr[0], K01 = nr[1], K02 = nr[2], K10 = nr[3], K11 = nr[4];
         const double K12 = nr[5], k0 = nr[6], k1 = nr[7];
         const double I00 = nr[8], I01 = nr[9], I11 = nr[10];
         {
-          const double* sn1 = sc + (t > 0 ? t - 1 : 0) * 11 * 64;
+          const double* sn1 = sc + (t > 0 ? t - 1 : 0) * NV * 64;
 #pragma unroll
           for (int e = 0; e < 11; e++) nr[e] = sn1[e * 64];
         }
@@ -501,16 +519,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       bool flipped = false;
       double rx = r64[0], ry = r64[64], rt = r64[2 * 64];
       int old_n = ap[0];
-      double ng[8];  // stage t + 1's gains, loaded while stage t computes
+      constexpr int NG = FST ? 14 : 8;
+      double ng[NG];  // stage t + 1's gains, loaded while stage t computes
 #pragma unroll
-      for (int e = 0; e < 8; e++) ng[e] = sc[e * 64];
+      for (int e = 0; e < NG; e++) ng[e] = sc[e * 64];
       for (int t = 0; t < m; t++) {
         const double K00 = ng[0], K01 = ng[1], K02 = ng[2], K10 = ng[3], K11 = ng[4];
-        const double K12 = ng[5], k0 = ng[6], k1 = ng[7];
+        const double K12 = ng[5];
+        const double k0 = FST ? ng[6] + ng[8] * lm0 + ng[9] * lm1 + ng[10] * lm2 : ng[6];
+        const double k1 = FST ? ng[7] + ng[11] * lm0 + ng[12] * lm1 + ng[13] * lm2 : ng[7];
         {
-          const double* sn1 = sc + (t + 1 < m ? t + 1 : m - 1) * 11 * 64;
+          const double* sn1 = sc + (t + 1 < m ? t + 1 : m - 1) * NV * 64;
 #pragma unroll
-          for (int e = 0; e < 8; e++) ng[e] = sn1[e * 64];
+          for (int e = 0; e < NG; e++) ng[e] = sn1[e * 64];
         }
         const int old = old_n;
         const double rxi = rx, ryi = ry, rti = rt;
@@ -606,9 +627,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     double x0 = xs0, x1 = xs1, x2 = xs2;
     for (int t = 0; t < m; t++) {
       const int i = s0 + t;
-      const double* s = sc + t * 11 * 64;
+      const double* s = sc + t * NV * 64;
       const double K00 = s[0], K01 = s[64], K02 = s[2 * 64], K10 = s[3 * 64], K11 = s[4 * 64];
-      const double K12 = s[5 * 64], k0 = s[6 * 64], k1 = s[7 * 64];
+      const double K12 = s[5 * 64];
+      const double k0 = FST ? s[6 * 64] + s[8 * 64] * lm0 + s[9 * 64] * lm1 + s[10 * 64] * lm2 : s[6 * 64];
+      const double k1 = FST ? s[7 * 64] + s[11 * 64] * lm0 + s[12 * 64] * lm1 + s[13 * 64] * lm2 : s[7 * 64];
       const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
       const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
       if (want_obj) {
@@ -695,15 +718,23 @@ hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const flo
                              const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   constexpr int L = 64 / S;
   const int waves = (B + L - 1) / L;
-  const size_t lds = seg_lds_bytes(P.N, S);
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&lane_seg_kernel<S, ROT>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL((lane_seg_kernel<S, ROT>), dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr, uo, xo,
-                     st, its, ws, lw.kmax, oo);
-  return hipGetLastError();
+  // the lam-gains stored (FST, no refresh sweep: measured C5 30.5 -> see DESIGN.md 2b') when the
+  // resident waves' LDS holds 14 doubles per stage, else the refresh sweep (11); lw.dref = 0
+  // forces the refresh (test hook, F110QP_LANE_DREF=0)
+  const size_t per_cu = ((size_t)waves + 255) / 256;
+  const bool fst = lw.dref && per_cu * seg_lds_bytes(P.N, S, true) <= 160 * 1024;
+  auto go = [&](auto kern, size_t lds) -> hipError_t {
+    if (lds > 64 * 1024) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr, uo, xo, st, its, ws,
+                       lw.kmax, oo);
+    return hipGetLastError();
+  };
+  return fst ? go(&lane_seg_kernel<S, ROT, true>, seg_lds_bytes(P.N, S, true))
+             : go(&lane_seg_kernel<S, ROT, false>, seg_lds_bytes(P.N, S, false));
 }
 
 }  // namespace f110qp

@@ -169,3 +169,19 @@ def test_segments_degenerate_bound(oracle, capi, monkeypatch):
         w = workload.make_batch(700, N, seed=4500, heading="true", lateral=0.0, steer_range=0.0)
         u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE, tol=2e-6, q=q)
         assert (st == capi.SOLVED).all()
+
+
+@pytest.mark.parametrize("S,N", [("4", 20), ("8", 40), ("2", 30)])
+def test_segments_refresh_and_stored_gains_agree(oracle, capi, monkeypatch, S, N):
+    """The two ways the segmented kernel applies the segment-end multiplier lam_j to the
+    feed-forward: the lam-gains F_i kept in the scratch (where the LDS holds 14 doubles per stage)
+    and the refresh sweep (F110QP_LANE_DREF=0 forces it): same status, solutions within 1e-6, both
+    at the exact optimum."""
+    monkeypatch.setenv("F110QP_LANE_SEG", S)
+    w = workload.make_batch(900, N, seed=7300 + N, heading="true", lateral=1.2, steer_range=0.8)
+    out = {}
+    for dref in ("1", "0"):
+        monkeypatch.setenv("F110QP_LANE_DREF", dref)
+        out[dref] = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
+    np.testing.assert_array_equal(out["0"][2], out["1"][2])
+    assert rel_err(out["1"][0], out["0"][0].astype(np.float64)).max() <= 1e-6
