@@ -76,6 +76,16 @@ __device__ __forceinline__ double seg_shfl(double v, int src) {
   return __shfl(v, src, 64);
 }
 
+#ifndef F110QP_SEG_NEWTON
+#define F110QP_SEG_NEWTON 2  // Newton steps after v_rcp_f64 in the masked 2x2 inverse (knob; 1
+                             // measured no change: C5 30.2, C2 27.3, C4 shard 63.7 us)
+#endif
+// unroll factor of the backward stage loop: 2 lets a stage's closed-loop map (Phi, psi, Gam)
+// overlap the next stage's Riccati step; same-box A/B C5 30.2 -> 29.6 us, C2 27.4 -> 26.9 at
+// S = 4, C4 shard (S = 8, m = 5) 63.6 -> 64.1, so S = 8 keeps 1 (knob F110QP_SEG_BW_UNROLL)
+#ifndef F110QP_SEG_BW_UNROLL
+#define F110QP_SEG_BW_UNROLL (S <= 4 ? 2 : 1)
+#endif
 #ifndef F110QP_SEG_WPE
 // waves-per-EU hint: 2 (<= 256 VGPRs; the grid still runs one wave per SIMD or CU) schedules
 // better than 1: same-box A/B C5 31.2 -> 30.6 us, C2 on the lane back end 28.3 -> 27.7, C4 shard
@@ -282,6 +292,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       int nst = ap[(m - 1) * 64];
       double rx = r64[(3 * (m - 1) + 0) * 64], ry = r64[(3 * (m - 1) + 1) * 64];
       double rt = r64[(3 * (m - 1) + 2) * 64];
+      constexpr int kBwUnroll = F110QP_SEG_BW_UNROLL;
+#pragma unroll kBwUnroll
       for (int t = m - 1; t >= 0; t--) {
         double* s = sc + t * NV * 64;
         const int sti = nst;
@@ -322,8 +334,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         const double M00 = f0 ? H00 : 1.0, M11 = f1 ? H11 : 1.0, M01 = (f0 && f1) ? H01 : 0.0;
         const double det = M00 * M11 - M01 * M01;
         double idet = __builtin_amdgcn_rcp(det);
-        idet = fma(idet, fma(-det, idet, 1.0), idet);
-        idet = fma(idet, fma(-det, idet, 1.0), idet);
+#pragma unroll
+        for (int nt = 0; nt < F110QP_SEG_NEWTON; nt++) idet = fma(idet, fma(-det, idet, 1.0), idet);
         const double I00 = f0 ? M11 * idet : 0.0, I11 = f1 ? M00 * idet : 0.0;
         const double I01 = (f0 && f1) ? -M01 * idet : 0.0;
         const double K00 = -I00 * X00 - I01 * X10, K01 = -I00 * X01 - I01 * X11;
