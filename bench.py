@@ -52,11 +52,19 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
 FP64_PEAK_TFLOPS = 78.6     # MI355X spec FP64 vector; tools/microbench/latency.hip measures the
                             # matching issue rate (one wave64 fp64 FMA per 4 cycles per SIMD)
-LANE_FLOPS_PER_STAGE = 290  # fp64 flops per stage and pass of lane_kernel (ISA count)
-# lane_seg_kernel (partitioned horizon): per stage and pass the backward stage with the segment's
-# closed-loop map (160 fp64 instructions), the feed-forward refresh (16) and the forward (35);
-# ~2.5 flops per instruction as above, the S - 1 segment steps (~200 fp64 each) spread per stage
+# fp64 flops per stage and PDAS pass of the sequential Riccati algorithm (lane_kernel.h, ISA count,
+# DESIGN.md 4): the algorithmic work of a pass, whatever kernel runs it. fp64_compute is priced on it.
+LANE_FLOPS_PER_STAGE = 290
+# lane_seg_kernel (partitioned horizon) executes more per stage and pass: the backward stage with the
+# segment's closed-loop map (160 fp64 instructions), the feed-forward refresh (16) and the forward
+# (35), ~2.5 flops per instruction, plus the S - 1 segment steps (~200 fp64 each) spread per stage.
+# That parallel-in-time redundancy is reported as "segmentation_overhead", never counted as work.
 SEG_FLOPS_PER_STAGE = 530
+
+
+def seg_flops_per_stage(S: int, N: int) -> float:
+    """fp64 flops the segmented kernel executes per stage and pass (redundancy included)."""
+    return SEG_FLOPS_PER_STAGE + 500.0 * (S - 1) / N * S
 
 
 def bytes_per_qp(N: int, gap: bool, warm: bool = False, backend: str = "wave") -> int:
@@ -517,10 +525,17 @@ def main():
     ms_per_step = el / args.steps * 1e3
     bpq = bytes_per_qp(N, gap, warm, be_name)
     # active-set size ~ iterations for an add-only run; use iterations as the upper bound
+    seg_overhead = None
     if be_name == "lane":
-        # Riccati + forward + adjoint sweeps: (active-set changes + 1) passes over N stages
-        fpq = (LANE_FLOPS_PER_STAGE if lane_seg == 1 else SEG_FLOPS_PER_STAGE + 500.0 * (lane_seg - 1) / N * lane_seg) \
-            * N * (float(itn.mean()) + 1.0)
+        # Riccati + forward + adjoint sweeps: (active-set changes + 1) passes over N stages, priced at
+        # the sequential algorithm's flops (the segmented kernel's redundancy is reported apart)
+        fpq = LANE_FLOPS_PER_STAGE * N * (float(itn.mean()) + 1.0)
+        if lane_seg > 1 and not gap:
+            seg_overhead = {"executed_flops_per_stage_pass": seg_flops_per_stage(lane_seg, N),
+                            "algorithmic_flops_per_stage_pass": LANE_FLOPS_PER_STAGE,
+                            "ratio": seg_flops_per_stage(lane_seg, N) / LANE_FLOPS_PER_STAGE,
+                            "note": "parallel-in-time redundancy of the partitioned horizon (closed-loop map "
+                                    "per stage, S - 1 segment steps); not counted in fp64_compute"}
         cpeak, cname = FP64_PEAK_TFLOPS, "fp64_compute"
     else:
         # pivots >= bounds active at the solution (each entered the active set once)
@@ -532,7 +547,10 @@ def main():
         cpeak, cname = FP32_PEAK_TFLOPS, "fp32_compute"
     achieved_gbs = bpq * Bper / (kms * 1e-3) / 1e9
     achieved_tf = fpq * Bper / (kms * 1e-3) / 1e12
-    traffic = load_traffic(args.config, Bper, N, be_name)
+    # the PMC summary's back-end key (tools/summarize_profiles.py KERNELS): the partitioned-horizon
+    # kernel is "lane_seg", the interior point (gap rows on the lane back end) "lane_ipm"
+    prof_be = be_name if be_name == "wave" else ("lane_ipm" if gap else ("lane_seg" if lane_seg > 1 else "lane"))
+    traffic = load_traffic(args.config, Bper, N, prof_be)
 
     out = {
         "metric": f"QP solves/s (horizon={N}, nx=3 reference model, nu=2)",
@@ -554,7 +572,9 @@ def main():
             "horizon": N,
             "gap_rows": bool(gap),
             "warm_start": bool(warm),
-            "backend": {"wave": "wave-per-QP (condensed, PDAS/GI)", "lane": "lane-per-QP (Riccati/PDAS fp64)"}[be_name]
+            "backend": {"wave": "wave-per-QP (condensed, PDAS/GI)",
+                        "lane": "lane-per-QP (Riccati interior point fp64 + GI hand-over)" if gap else
+                                "lane-per-QP (Riccati/PDAS fp64)"}[be_name]
                        + (" grouped: one W = H^-1 per scenario" if grouped and be_name == "wave" else ""),
             **({"lane_qps_per_wave": lane_qpw, "lane_scratch": capi.SCRATCH_NAMES[lane_scr],
                 "lane_segments": lane_seg}
@@ -585,13 +605,16 @@ def main():
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
             "kernel": {"wave": "f110qp::solve_kernel",
-                       "lane": ("f110qp::lane_kernel" if lane_seg == 1 else
-                                f"f110qp::lane_seg_kernel<{lane_seg}> (partitioned horizon)")
-                               + " (the only launch of the step)"}[be_name],
+                       "lane": (f"f110qp::lane_ipm_kernel<{lane_seg}> (interior point) + the wave kernel over its "
+                                "hand-over list" if gap else
+                                ("f110qp::lane_kernel" if lane_seg == 1 else
+                                 f"f110qp::lane_seg_kernel<{lane_seg}> (partitioned horizon)")
+                                + " (the only launch of the step)")}[be_name],
             "kernel_ms_per_launch": kms,
             "algorithmic_bytes_per_qp": bpq,
             cname: {"achieved": achieved_tf, "peak": cpeak, "unit": "TFLOP/s",
                     "frac": achieved_tf / cpeak, "flops_per_qp": fpq},
+            **({"segmentation_overhead": seg_overhead} if seg_overhead else {}),
             "note": ("lane kernel: fp64 VALU-issue and scratch-latency bound (Riccati sweeps, 64 QPs per "
                      "wave); traffic = PMC HBM bytes incl. the Riccati scratch" if be_name == "lane" and lane_seg == 1 else
                      f"partitioned-horizon lane kernel: one QP per {lane_seg} lanes, latency-bound by the slowest "

@@ -97,6 +97,8 @@ struct f110qp_ctx {
   DevBuf gW, gkey, glead;    // grouped mode: W = H^-1, key and leader per group
   DevBuf dgrp;               // host-pointer grouped calls: device copy of the group ids
   DevBuf lscr;               // lane back end: HBM Riccati scratch (when not in LDS)
+  DevBuf hand;               // lane back end, gap rows: hand-over count + list (B + 1 ints)
+  f110qp::IpmKnobs ipm;      // lane back end, gap rows: interior-point knobs (test/bench hooks)
   int lane_kmax = 16;        // lane back end: PDAS passes before single (least-index) flips
   int lane_mode = 0;         // lane scratch placement (LaneWork::mode)
   int lane_qpw = 0;          // lane QPs per wave (LaneWork::qpw, 0 = auto)
@@ -196,6 +198,26 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     const int v = std::atoi(es);
     if (v == 0 || v == 1 || v == 2 || v == 4 || v == 8) c->lane_seg = v;
   }
+  c->ipm.tolp = c->ipm.told = 1e-8;
+  // test/bench hooks of the interior-point lane kernel (gap rows): polish threshold on mu,
+  // acceptance tolerance, iteration cap before the hand-over to the wave kernel
+  if (const char* ev = std::getenv("F110QP_IPM_POLMU")) {
+    const double v = std::atof(ev);
+    if (v > 0.0) c->ipm.pol_mu = v;
+  }
+  if (const char* ev = std::getenv("F110QP_IPM_TOL")) {
+    const double v = std::atof(ev);
+    if (v > 0.0 && v < 1e-3) c->ipm.tolp = c->ipm.told = v;
+  }
+  if (const char* ev = std::getenv("F110QP_IPM_MAXIT")) {
+    const int v = std::atoi(ev);
+    if (v >= 0 && v <= 200) c->ipm.max_iter = v;
+  }
+  if (const char* ev = std::getenv("F110QP_IPM_DEBUG")) c->ipm.debug = std::atoi(ev);
+  if (const char* ev = std::getenv("F110QP_IPM_SFLOOR")) {
+    const double v = std::atof(ev);
+    if (v > 0.0) c->ipm.s_floor = v;
+  }
   // test hook: F110QP_PDAS_MAX caps the wave kernel's box PDAS passes (0 = GI from scratch)
   k.pdas_max = 10;
   if (const char* ep = std::getenv("F110QP_PDAS_MAX")) {
@@ -214,6 +236,7 @@ void f110qp_destroy(f110qp_ctx* c) {
   c->hin.release(); c->hout.release(); c->din.release(); c->dout.release();
   c->wW.release(); c->wkey.release(); c->wact.release();
   c->lscr.release();
+  c->hand.release();
   c->gW.release(); c->gkey.release(); c->glead.release(); c->dgrp.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -255,33 +278,55 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
   return F110QP_OK;
 }
 
-// Back end of a call and, for the lane back end, its workspace.
-static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110qp::LaneWork* lw,
-                     bool grouped = false) {
-  *lw = f110qp::LaneWork();
+// The back end a call of `batch` QPs runs on (what AUTO resolves to). Box rows: the lane back end
+// from F110QP_LANE_MIN_BATCH[_WIDE]. Gap rows: AUTO keeps the wave kernel (its GI measured 290 us
+// on C3 against 1,010 us for the lane interior point); an explicit
+// F110QP_BACKEND_LANE runs the interior point wherever its LDS fits (lane_ipm_segments > 0), else
+// the wave kernel.
+static int resolve_backend(f110qp_ctx* c, int batch, bool grouped, const f110qp::LaneWork& lw) {
   const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
   int be = c->cfg.backend;
+  if (gap) {
+    if (be != F110QP_BACKEND_LANE) return F110QP_BACKEND_WAVE;
+    return f110qp::lane_ipm_segments(c->kp, batch, lw) > 0 ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
+  }
   if (be == F110QP_BACKEND_AUTO) {
     const int min_b = grouped ? (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH_GROUPED
                                                       : F110QP_LANE_MIN_BATCH_GROUPED_WIDE)
                               : (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH : F110QP_LANE_MIN_BATCH_WIDE);
-    be = (!gap && batch >= min_b) ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
+    be = batch >= min_b ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
   }
-  if (gap) be = F110QP_BACKEND_WAVE;
-  *backend = (be == F110QP_BACKEND_LANE) ? f110qp::BACKEND_LANE : f110qp::BACKEND_WAVE;
-  if (*backend == f110qp::BACKEND_WAVE) return F110QP_OK;
-  // HBM scratch of ceil(B/L) waves x N stages x 8 values x L lanes (<= (B + 63) x N x 8 doubles)
-  (void)s;
-  const size_t N = (size_t)c->cfg.horizon;
-  hipError_t e = c->lscr.ensure(((size_t)batch + 63) * N * 8 * sizeof(double));
-  if (e != hipSuccess) return hip_fail(e, "hipMalloc lane workspace");
-  lw->scratch = (double*)c->lscr.p;
+  return be;
+}
+
+// Back end of a call and, for the lane back end, its workspace.
+static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110qp::LaneWork* lw,
+                     bool grouped = false) {
+  *lw = f110qp::LaneWork();
   lw->kmax = c->lane_kmax;
   lw->mode = c->lane_mode;
   lw->qpw = c->lane_qpw;
   lw->rot = c->lane_rot;
   lw->dref = c->lane_dref;
   lw->seg = c->lane_seg;
+  lw->ipm = c->ipm;
+  *backend = resolve_backend(c, batch, grouped, *lw) == F110QP_BACKEND_LANE ? f110qp::BACKEND_LANE
+                                                                           : f110qp::BACKEND_WAVE;
+  if (*backend == f110qp::BACKEND_WAVE) return F110QP_OK;
+  (void)s;
+  hipError_t e;
+  if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) {
+    // hand-over count + list of the interior-point kernel
+    if ((e = c->hand.ensure(((size_t)batch + 1) * sizeof(int))) != hipSuccess)
+      return hip_fail(e, "hipMalloc hand-over list");
+    lw->hand = (int*)c->hand.p;
+    return F110QP_OK;
+  }
+  // HBM scratch of ceil(B/L) waves x N stages x 8 values x L lanes (<= (B + 63) x N x 8 doubles)
+  const size_t N = (size_t)c->cfg.horizon;
+  e = c->lscr.ensure(((size_t)batch + 63) * N * 8 * sizeof(double));
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc lane workspace");
+  lw->scratch = (double*)c->lscr.p;
   return F110QP_OK;
 }
 
@@ -410,23 +455,16 @@ int f110qp_backend_info(f110qp_ctx* c, int batch, int grouped, int* backend, int
   if (!c) return fail(F110QP_ERR_INVALID, "ctx is NULL");
   if (batch < 1) return fail(F110QP_ERR_INVALID, "batch must be >= 1");
   const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
-  int be = c->cfg.backend;
-  if (be == F110QP_BACKEND_AUTO) {
-    const int min_b = grouped ? (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH_GROUPED
-                                                      : F110QP_LANE_MIN_BATCH_GROUPED_WIDE)
-                              : (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH : F110QP_LANE_MIN_BATCH_WIDE);
-    be = (!gap && batch >= min_b) ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
-  }
-  if (gap) be = F110QP_BACKEND_WAVE;
   f110qp::LaneWork lw;
   lw.mode = c->lane_mode;
   lw.qpw = c->lane_qpw;
   lw.seg = c->lane_seg;
+  const int be = resolve_backend(c, batch, grouped != 0, lw);
   const bool lane = be == F110QP_BACKEND_LANE;
-  const int segs = lane ? f110qp::lane_segments(c->kp, batch, lw) : 1;
+  const int segs = lane ? (gap ? f110qp::lane_ipm_segments(c->kp, batch, lw) : f110qp::lane_segments(c->kp, batch, lw)) : 1;
   if (backend) *backend = be;
   if (qps_per_wave) *qps_per_wave = lane ? (segs > 1 ? 64 / segs : f110qp::lane_qps_per_wave(batch, lw.qpw)) : 1;
-  if (scratch) *scratch = lane ? (segs > 1 ? 1 : f110qp::lane_scratch_mode(c->kp, batch, lw)) : 0;
+  if (scratch) *scratch = lane ? (segs > 1 || gap ? 1 : f110qp::lane_scratch_mode(c->kp, batch, lw)) : 0;
   return F110QP_OK;
 }
 
@@ -440,7 +478,9 @@ int f110qp_lane_segments(f110qp_ctx* c, int batch, int* segments) {
   lw.mode = c->lane_mode;
   lw.qpw = c->lane_qpw;
   lw.seg = c->lane_seg;
-  *segments = be == F110QP_BACKEND_LANE ? f110qp::lane_segments(c->kp, batch, lw) : 1;
+  if (be != F110QP_BACKEND_LANE) *segments = 1;
+  else if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) *segments = f110qp::lane_ipm_segments(c->kp, batch, lw);
+  else *segments = f110qp::lane_segments(c->kp, batch, lw);
   return F110QP_OK;
 }
 

@@ -45,6 +45,17 @@ struct WarmState {
   int ngroups = 0;
 };
 
+// Knobs of the interior-point lane kernel for QPs with gap rows (lane_ipm_kernel.h).
+struct IpmKnobs {
+  double pol_mu = 1e-3;  // polish once a QP's mu (mean complementarity) is below this
+  double tolp = 1e-9;    // polish acceptance: row violation, x (1 + |bound|)
+  double told = 1e-9;    // polish acceptance: multiplier sign of an active row
+  double tau = 0.995;    // fraction to the boundary
+  double s_floor = 1.0;  // initial slack floor
+  int max_iter = 30;     // interior-point iterations before the hand-over to the wave kernel
+  int debug = 0;         // test hook: return every QP's current iterate as SOLVED (no polish test)
+};
+
 // Workspace of the lane-per-QP kernel (lane_kernel.h): the HBM Riccati scratch when it does
 // not stay in LDS (ceil(B/L) x N x 8 x L doubles at most, L QPs per wave <= 64).
 struct LaneWork {
@@ -55,6 +66,8 @@ struct LaneWork {
   int rot = 1;    // 1: heading-frame kernel when q0 == q1 (lane_kernel.h ROT); 0: general frame
   int dref = 1;   // 1: fp64 references in LDS when the resident waves fit (DREF); 0: float
   int seg = 0;    // horizon segments per QP (lane_seg_kernel.h): 0 auto, 1 off, 2 / 4 / 8 forced
+  int* hand = nullptr;  // gap rows: hand-over count (hand[0]) + list (hand + 1, B ints)
+  IpmKnobs ipm;
 };
 
 // Optional per-QP objective outputs (fp64, computed in the kernels' output sweeps from the fp64
@@ -75,10 +88,22 @@ int lane_scratch_mode(const KParams& P, int B, const LaneWork& lw);
 // group of 64 / L identical lanes; S > 1 = lane_seg_kernel.h, 64 / S QPs per wave)
 int lane_segments(const KParams& P, int B, const LaneWork& lw);
 
+// Horizon segments per QP of the interior-point lane kernel for a batch WITH gap rows
+// (lane_ipm_kernel.h), or 0 when its LDS does not fit (the wave kernel then takes the batch).
+int lane_ipm_segments(const KParams& P, int B, const LaneWork& lw);
+
+// The interior-point lane kernel alone: QPs it does not polish are appended to the hand-over
+// list (lw.hand; the count must be zero on entry).
+hipError_t launch_lane_ipm(const KParams& P, int B, const float* x0, const float* u_lin,
+                           const float* x_ref, const float* hs, float* u_out, float* x_out,
+                           int* status, int* iters, const LaneWork& lw, const ObjOut& oo,
+                           hipStream_t stream);
+
 enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
 
-// Solve B QPs. hs == nullptr -> box-only kernels (gap rows inactive). backend LANE (box rows
-// only): the lane-per-QP Riccati/PDAS kernel alone (one launch, no hand-over).
+// Solve B QPs. hs == nullptr -> box-only kernels (gap rows inactive). backend LANE: box rows, the
+// lane-per-QP Riccati/PDAS kernel alone (one launch, no hand-over); gap rows, the interior-point
+// lane kernel, then the wave kernel over its hand-over list (QPs it did not polish).
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u_lin,
                         const float* x_ref, const float* hs, float* u_out, float* x_out,
                         int* status, int* iters, const WarmState& warm, int backend,

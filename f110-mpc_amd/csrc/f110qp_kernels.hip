@@ -35,11 +35,23 @@ static hipError_t launch_g(const KParams& P, int B, const float* x0, const float
   return hipErrorInvalidValue;
 }
 
+// waves of the hand-over launch (a work loop over the list; one per CU)
+constexpr int kHandGrid = 256;
+
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
                         const float* xr, const float* hs, float* uo, float* xo, int* st,
                         int* its, const WarmState& ws, int backend, const LaneWork& lw,
                         const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
+  if (hs && backend == BACKEND_LANE) {
+    // interior point on the lane back end, then the wave kernel's GI over the QPs it handed over
+    // (none in the common case: every wave of that launch reads the zero count and exits)
+    hipError_t e = hipMemsetAsync(lw.hand, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+    if ((e = launch_lane_ipm(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s)) != hipSuccess) return e;
+    return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 1,
+                          lw.hand, B < kHandGrid ? B : kHandGrid, oo, s);
+  }
   if (hs)
     return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
                           nullptr, B, oo, s);
@@ -76,7 +88,7 @@ hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const 
                                 int* its, const WarmState& gws, int* leader, int backend,
                                 const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (!hs && backend == BACKEND_LANE)  // per-QP Riccati: nothing to share
+  if (backend == BACKEND_LANE)  // per-QP Riccati / interior point: nothing to share
     return launch_solve(P, B, x0, ul, xr, hs, uo, xo, st, its, WarmState(), backend, lw, oo, s);
   hipError_t e = hipMemsetAsync(leader, 0x7f, (size_t)gws.ngroups * sizeof(int), s);
   if (e != hipSuccess) return e;
