@@ -105,6 +105,7 @@ struct f110qp_ctx {
   int lane_rot = 1;          // lane heading-frame kernel when q0 == q1 (LaneWork::rot)
   int lane_dref = 1;         // lane fp64 references in LDS when they fit (LaneWork::dref)
   int lane_seg = 0;          // lane horizon segments per QP (LaneWork::seg: 0 auto, 1 off, 2/4/8)
+  int lane_seg32 = 0;        // segmented kernel: force fp32 references + scratch (LaneWork::seg32)
   hipStream_t stream = nullptr;
 };
 
@@ -218,6 +219,8 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     const double v = std::atof(ev);
     if (v > 0.0) c->ipm.s_floor = v;
   }
+  // test hook: F110QP_LANE_SEG_F32=1 forces the segmented kernel's float references and scratch
+  if (const char* ef = std::getenv("F110QP_LANE_SEG_F32")) c->lane_seg32 = std::atoi(ef) != 0;
   // test hook: F110QP_PDAS_MAX caps the wave kernel's box PDAS passes (0 = GI from scratch)
   k.pdas_max = 10;
   if (const char* ep = std::getenv("F110QP_PDAS_MAX")) {
@@ -309,6 +312,7 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   lw->rot = c->lane_rot;
   lw->dref = c->lane_dref;
   lw->seg = c->lane_seg;
+  lw->seg32 = c->lane_seg32;
   lw->ipm = c->ipm;
   *backend = resolve_backend(c, batch, grouped, *lw) == F110QP_BACKEND_LANE ? f110qp::BACKEND_LANE
                                                                            : f110qp::BACKEND_WAVE;
@@ -464,7 +468,10 @@ int f110qp_backend_info(f110qp_ctx* c, int batch, int grouped, int* backend, int
   const int segs = lane ? (gap ? f110qp::lane_ipm_segments(c->kp, batch, lw) : f110qp::lane_segments(c->kp, batch, lw)) : 1;
   if (backend) *backend = be;
   if (qps_per_wave) *qps_per_wave = lane ? (segs > 1 ? 64 / segs : f110qp::lane_qps_per_wave(batch, lw.qpw)) : 1;
-  if (scratch) *scratch = lane ? (segs > 1 || gap ? 1 : f110qp::lane_scratch_mode(c->kp, batch, lw)) : 0;
+  lw.seg32 = c->lane_seg32;
+  if (scratch)
+    *scratch = !lane ? 0 : gap ? 1 : segs > 1 ? f110qp::lane_seg_scratch(c->kp, batch, segs, lw)
+                                              : f110qp::lane_scratch_mode(c->kp, batch, lw);
   return F110QP_OK;
 }
 

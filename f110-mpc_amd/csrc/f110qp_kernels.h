@@ -66,6 +66,7 @@ struct LaneWork {
   int rot = 1;    // 1: heading-frame kernel when q0 == q1 (lane_kernel.h ROT); 0: general frame
   int dref = 1;   // 1: fp64 references in LDS when the resident waves fit (DREF); 0: float
   int seg = 0;    // horizon segments per QP (lane_seg_kernel.h): 0 auto, 1 off, 2 / 4 / 8 forced
+  int seg32 = 0;  // segmented kernel: 1 forces float references and Riccati scratch in LDS
   int* hand = nullptr;  // gap rows: hand-over count (hand[0]) + list (hand + 1, B ints)
   IpmKnobs ipm;
 };
@@ -87,6 +88,8 @@ int lane_scratch_mode(const KParams& P, int B, const LaneWork& lw);
 // horizon segments per QP the lane launch picks for a batch (1 = lane_kernel.h, one QP per lane
 // group of 64 / L identical lanes; S > 1 = lane_seg_kernel.h, 64 / S QPs per wave)
 int lane_segments(const KParams& P, int B, const LaneWork& lw);
+// scratch of the segmented kernel at S segments: 1 LDS fp64, 2 LDS fp32 (lane_seg_kernel.h)
+int lane_seg_scratch(const KParams& P, int B, int S, const LaneWork& lw);
 
 // Horizon segments per QP of the interior-point lane kernel for a batch WITH gap rows
 // (lane_ipm_kernel.h), or 0 when its LDS does not fit (the wave kernel then takes the batch).

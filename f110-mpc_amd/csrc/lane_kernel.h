@@ -637,8 +637,12 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
 #pragma unroll
             for (int e = 0; e < 8; e++) ur[t][e] = s[e * ES];
           }
-          const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
-          const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
+          // fp32 gains: a free input may sit outside its box by the single-flip tolerance
+          // (1e-6 scaled); the output clamps it, x* is the rollout of the clamped u*
+          const double u0 = F32 ? fmin(fmax(K00 * x0 + K01 * x1 + K02 * x2 + k0, lb0), ub0)
+                                : K00 * x0 + K01 * x1 + K02 * x2 + k0;
+          const double u1 = F32 ? fmin(fmax(K10 * x0 + K11 * x1 + K12 * x2 + k1, lb1), ub1)
+                                : K10 * x0 + K11 * x1 + K12 * x2 + k1;
           const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
           const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;
           const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
@@ -682,8 +686,10 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
       const ST* s = sp + (size_t)i * 8 * L;
       const double K00 = s[0], K01 = s[ES], K02 = s[2 * ES], K10 = s[3 * ES];
       const double K11 = s[4 * ES], K12 = s[5 * ES], k0 = s[6 * ES], k1 = s[7 * ES];
-      const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
-      const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
+      const double u0 = F32 ? fmin(fmax(K00 * x0 + K01 * x1 + K02 * x2 + k0, lb0), ub0)
+                            : K00 * x0 + K01 * x1 + K02 * x2 + k0;
+      const double u1 = F32 ? fmin(fmax(K10 * x0 + K11 * x1 + K12 * x2 + k1, lb1), ub1)
+                            : K10 * x0 + K11 * x1 + K12 * x2 + k1;
       J += 0.5 * (r0 * (u0 - ud0) * (u0 - ud0) + r1 * (u1 - ud1) * (u1 - ud1));
       const double nx0 = ROT ? x0 + b00 * u0 : x0 + a02 * x2 + b00 * u0 + c0;
       const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;

@@ -15,13 +15,18 @@ template <int S, bool ROT>
 hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                              float* uo, float* xo, int* st, int* its, const WarmState& ws,
                              const LaneWork& lw, const ObjOut& oo, hipStream_t s);  // lane_seg_inst.hip
-constexpr size_t seg_lds_per_wave(int N, int S) { return (size_t)((N + S - 1) / S) * 64 * (3 * 8 + 4 + 11 * 8); }
+// LDS per wave of the segmented kernel with fp64 / fp32 references and scratch (lane_seg_kernel.h
+// seg_lds_bytes without the lam-gains)
+constexpr size_t seg_lds_per_wave(int N, int S, bool f32 = false) {
+  return (size_t)((N + S - 1) / S) * 64 * (3 * (f32 ? 4 : 8) + 4 + 11 * (f32 ? 4 : 8));
+}
 
 // Horizon segments per QP (lane_seg_kernel.h). A batch whose waves leave SIMDs idle (the QPs fit
 // in fewer than one wave per SIMD at 64 / S QPs per wave) splits every QP's horizon over S lanes
 // instead of running 64 / L identical copies of it. S cuts N into segments of >= 2 stages (of
 // floor(N / S) or one more), the grid stays within one wave per SIMD (1,024 waves) and the
-// segmented LDS fits. Among those the launch takes the S with the shortest per-pass chain by the
+// segmented LDS fits (fp64 references and scratch, or float ones where fp64 does not fit:
+// 16,384 x N = 40 runs S = 4 on fp32 scratch, round 4). Among those the launch takes the S with the shortest per-pass chain by the
 // instruction model of DESIGN.md 2b': sequential N x ~255 instructions, segmented ceil(N / S) x
 // ~350 + (S - 1) x ~230 (the two segment recursions). A forced QPs-per-wave or scratch placement
 // keeps lane_kernel.h.
@@ -31,7 +36,7 @@ int lane_segments(const KParams& P, int B, const LaneWork& lw) {
     if (N / S < 2) return false;
     const size_t waves = ((size_t)B * S + 63) / 64;
     const size_t per_cu = (waves + 255) / 256;
-    return per_cu <= 4 && per_cu * seg_lds_per_wave(N, S) <= 160 * 1024;
+    return per_cu <= 4 && per_cu * seg_lds_per_wave(N, S, true) <= 160 * 1024;
   };
   if (lw.seg == 1) return 1;
   if (lw.seg == 2 || lw.seg == 4 || lw.seg == 8) return fits(lw.seg) ? lw.seg : 1;

@@ -15,4 +15,6 @@ F110QP_SEG_INST(4, false)
 F110QP_SEG_INST(8, true)
 F110QP_SEG_INST(8, false)
 #undef F110QP_SEG_INST
+
+int lane_seg_scratch(const KParams& P, int B, int S, const LaneWork& lw) { return seg_scratch_mode(P, B, S, lw); }
 }  // namespace f110qp

@@ -62,8 +62,10 @@ __device__ unsigned long long g_sstamps[4096 * kSegStampSlots];
 // LDS bytes per wave of the segmented kernel for horizon N split into S segments (rows for the
 // longest segment, ceil(N / S) stages)
 // FST: the scratch keeps the lam-gains F_i (6) instead of S_i^-1 (3): 14 doubles per stage
-constexpr size_t seg_lds_bytes(int N, int S, bool fst = false) {
-  return (size_t)((N + S - 1) / S) * 64 * (3 * 8 + 4 + (fst ? 14 : 11) * 8);
+// F32: references and Riccati scratch held as float (the fp64 arithmetic is unchanged): 60 instead
+// of 116 bytes per stage and lane, so 16,384 x N = 40 QPs per GPU fit at S = 4 (DESIGN.md 2b')
+constexpr size_t seg_lds_bytes(int N, int S, bool fst = false, bool f32 = false) {
+  return (size_t)((N + S - 1) / S) * 64 * (3 * (f32 ? 4 : 8) + 4 + (fst ? 14 : 11) * (f32 ? 4 : 8));
 }
 
 template <int M>
@@ -92,7 +94,7 @@ __device__ __forceinline__ double seg_shfl(double v, int src) {
 // neutral (tools/ab_seg_variant.sh)
 #define F110QP_SEG_WPE 2
 #endif
-template <int S, bool ROT, bool FST>
+template <int S, bool ROT, bool FST, typename ST = double>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_WPE, F110QP_SEG_WPE))) void lane_seg_kernel(
     const KParams P, const int B, const float* __restrict__ x0g, const float* __restrict__ ulg,
     const float* __restrict__ xrg, float* __restrict__ uout, float* __restrict__ xout,
@@ -123,9 +125,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
 #ifdef F110QP_STAMPS
   unsigned long long acc_bw = 0, acc_dual = 0, acc_ref = 0, acc_fw = 0, t_setup = 0, npass = 0;
 #endif
-  double* const r64 = seg_smem + lane;                                     // [3mM][64]
-  int* const ap = reinterpret_cast<int*>(seg_smem + 3 * mM * 64) + lane;  // [mM][64]
-  double* const sc = seg_smem + 3 * mM * 64 + mM * 32 + lane;             // [mM][NV][64]
+  constexpr bool F32 = sizeof(ST) == 4;
+  char* const lbase = reinterpret_cast<char*>(seg_smem);
+  const size_t o_ap = (size_t)3 * mM * 64 * sizeof(ST), o_sc = o_ap + (size_t)mM * 64 * 4;
+  ST* const r64 = reinterpret_cast<ST*>(lbase) + lane;                     // [3mM][64]
+  int* const ap = reinterpret_cast<int*>(lbase + o_ap) + lane;             // [mM][64]
+  ST* const sc = reinterpret_cast<ST*>(lbase + o_sc) + lane;               // [mM][NV][64]
 
   // per-QP inputs and the warm-start key, issued before the staging loads so that both share
   // one HBM round trip
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   // valid address (clamped) and every store lands (past the staged rows for e >= tot), so the
   // loop has no EXEC-masked region: ~11 instructions per element instead of ~50 (ISA).
   {
-    float* stg = reinterpret_cast<float*>(seg_smem + 3 * mM * 64 + mM * 32);
+    float* stg = reinterpret_cast<float*>(lbase + o_sc);
     const int n3 = 3 * N, S3 = 3 * P.xr_stride, tot = nq * n3;
     const float* src = xrg + (size_t)b0 * S3;
     const int dq = 64 / n3, dc = 64 - dq * n3;
@@ -192,19 +197,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   const double ud0 = P.udes[0], ud1 = P.udes[1];
   const double lb0 = (double)P.umin[0], lb1 = (double)P.umin[1];
   const double ub0 = (double)P.umax[0], ub1 = (double)P.umax[1];
-  // PDAS flip tolerances of lane_kernel.h's fp64-scratch kernels (1e-10, scaled)
-  const double pt = 1e-10, gt = 1e-10;
-  const double lbe0 = lb0 - pt * (1.0 + fabs(lb0)), ube0 = ub0 + pt * (1.0 + fabs(ub0));
-  const double lbe1 = lb1 - pt * (1.0 + fabs(lb1)), ube1 = ub1 + pt * (1.0 + fabs(ub1));
-  const double gtol0 = gt * (1.0 + r0 * (1.0 + fabs(lb0) + fabs(ub0)));
-  const double gtol1 = gt * (1.0 + r1 * (1.0 + fabs(lb1) + fabs(ub1)));
+  // PDAS flip tolerances of lane_kernel.h: fp64 scratch 1e-10 (scaled) in every pass; fp32
+  // scratch (gains rounded to ~1e-7) exact compares in the PDAS passes and 1e-6 / 1e-5 in the
+  // single-flip passes, where a degenerate bound then settles
+  const double ptT = F32 ? 0.0 : 1e-10, gtT = F32 ? 0.0 : 1e-10;
+  const double ptL = F32 ? 1e-6 : 1e-10, gtL = F32 ? 1e-5 : 1e-10;
+  const double lbe0 = lb0 - ptT * (1.0 + fabs(lb0)), ube0 = ub0 + ptT * (1.0 + fabs(ub0));
+  const double lbe1 = lb1 - ptT * (1.0 + fabs(lb1)), ube1 = ub1 + ptT * (1.0 + fabs(ub1));
+  const double gtol0 = gtT * (1.0 + r0 * (1.0 + fabs(lb0) + fabs(ub0)));
+  const double gtol1 = gtT * (1.0 + r1 * (1.0 + fabs(lb1) + fabs(ub1)));
+  const double lbl0 = lb0 - ptL * (1.0 + fabs(lb0)), ubl0 = ub0 + ptL * (1.0 + fabs(ub0));
+  const double lbl1 = lb1 - ptL * (1.0 + fabs(lb1)), ubl1 = ub1 + ptL * (1.0 + fabs(ub1));
+  const double gtoll0 = gtL * (1.0 + r0 * (1.0 + fabs(lb0) + fabs(ub0)));
+  const double gtoll1 = gtL * (1.0 + r1 * (1.0 + fabs(lb1) + fabs(ub1)));
 
   SSTAMP(t_lin);
   // references of the lane's stages: recentred (ROT: rotated) fp64, lane-major; a non-finite
   // entry flags the QP (one ballot folded over its segment lanes)
   bool nonfin = false;
   {
-    const float* stg = reinterpret_cast<const float*>(seg_smem + 3 * mM * 64 + mM * 32);
+    const float* stg = reinterpret_cast<const float*>(lbase + o_sc);
     for (int t = 0; t < m; t++) {
       const int i = s0 + t;
       const float fx = stg[(3 * i + 0) * L + slot], fy = stg[(3 * i + 1) * L + slot];
@@ -295,7 +307,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       constexpr int kBwUnroll = F110QP_SEG_BW_UNROLL;
 #pragma unroll kBwUnroll
       for (int t = m - 1; t >= 0; t--) {
-        double* s = sc + t * NV * 64;
+        ST* s = sc + t * NV * 64;
         const int sti = nst;
         const int tn = t > 0 ? t - 1 : 0;
         nst = ap[tn * 64];
@@ -495,12 +507,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
 #pragma unroll
       for (int e = 0; e < 11; e++) nr[e] = sc[((m - 1) * NV + e) * 64];
       for (int t = m - 1; t >= 0; t--) {
-        double* s = sc + t * NV * 64;
+        ST* s = sc + t * NV * 64;
         const double K00 = nr[0], K01 = nr[1], K02 = nr[2], K10 = nr[3], K11 = nr[4];
         const double K12 = nr[5], k0 = nr[6], k1 = nr[7];
         const double I00 = nr[8], I01 = nr[9], I11 = nr[10];
         {
-          const double* sn1 = sc + (t > 0 ? t - 1 : 0) * NV * 64;
+          const ST* sn1 = sc + (t > 0 ? t - 1 : 0) * NV * 64;
 #pragma unroll
           for (int e = 0; e < 11; e++) nr[e] = sn1[e * 64];
         }
@@ -543,7 +555,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         const double k0 = FST ? ng[6] + ng[8] * lm0 + ng[9] * lm1 + ng[10] * lm2 : ng[6];
         const double k1 = FST ? ng[7] + ng[11] * lm0 + ng[12] * lm1 + ng[13] * lm2 : ng[7];
         {
-          const double* sn1 = sc + (t + 1 < m ? t + 1 : m - 1) * NV * 64;
+          const ST* sn1 = sc + (t + 1 < m ? t + 1 : m - 1) * NV * 64;
 #pragma unroll
           for (int e = 0; e < NG; e++) ng[e] = sn1[e * 64];
         }
@@ -569,9 +581,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         for (int a = 0; a < 2; a++) {
           const int ca = (old >> (2 * a)) & 3;
           const double u = a ? u1 : u0, g = a ? g1 : g0;
-          const double gta = a ? gtol1 : gtol0;
-          const bool nlo = ((ca == 1) & (g > -gta)) | ((ca == 0) & (u < (a ? lbe1 : lbe0)));
-          const bool nhi = !nlo & (((ca == 2) & (g < gta)) | ((ca == 0) & (u > (a ? ube1 : ube0))));
+          const double gta = MODE ? (a ? gtoll1 : gtoll0) : (a ? gtol1 : gtol0);
+          const double lbx = MODE ? (a ? lbl1 : lbl0) : (a ? lbe1 : lbe0);
+          const double ubx = MODE ? (a ? ubl1 : ubl0) : (a ? ube1 : ube0);
+          const bool nlo = ((ca == 1) & (g > -gta)) | ((ca == 0) & (u < lbx));
+          const bool nhi = !nlo & (((ca == 2) & (g < gta)) | ((ca == 0) & (u > ubx)));
           const int nca = (int)nlo | ((int)nhi << 1);
           if constexpr (MODE == 0) {
             st |= nca << (2 * a);
@@ -641,13 +655,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     double x0 = xs0, x1 = xs1, x2 = xs2;
     for (int t = 0; t < m; t++) {
       const int i = s0 + t;
-      const double* s = sc + t * NV * 64;
+      const ST* s = sc + t * NV * 64;
       const double K00 = s[0], K01 = s[64], K02 = s[2 * 64], K10 = s[3 * 64], K11 = s[4 * 64];
       const double K12 = s[5 * 64];
       const double k0 = FST ? s[6 * 64] + s[8 * 64] * lm0 + s[9 * 64] * lm1 + s[10 * 64] * lm2 : s[6 * 64];
       const double k1 = FST ? s[7 * 64] + s[11 * 64] * lm0 + s[12 * 64] * lm1 + s[13 * 64] * lm2 : s[7 * 64];
-      const double u0 = K00 * x0 + K01 * x1 + K02 * x2 + k0;
-      const double u1 = K10 * x0 + K11 * x1 + K12 * x2 + k1;
+      // fp32 scratch: clamp a free input that sits outside its box by the single-flip tolerance
+      const double u0 = F32 ? fmin(fmax(K00 * x0 + K01 * x1 + K02 * x2 + k0, lb0), ub0)
+                            : K00 * x0 + K01 * x1 + K02 * x2 + k0;
+      const double u1 = F32 ? fmin(fmax(K10 * x0 + K11 * x1 + K12 * x2 + k1, lb1), ub1)
+                            : K10 * x0 + K11 * x1 + K12 * x2 + k1;
       if (want_obj) {
         qterm(r64[(3 * t) * 64], r64[(3 * t + 1) * 64], r64[(3 * t + 2) * 64], x0, x1, x2);
         J += 0.5 * (r0 * (u0 - ud0) * (u0 - ud0) + r1 * (u1 - ud1) * (u1 - ud1));
@@ -726,17 +743,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
 #endif
 }
 
+// Scratch of the segmented kernel for a batch: 1 fp64 (the lam-gains kept when they fit), 2 fp32
+// (references and scratch as float) when fp64 does not fit the CU's 160 KiB at the grid's waves
+// per CU, or when forced (lw.seg32: F110QP_LANE_SEG_F32=1); 0 if neither fits.
+inline int seg_scratch_mode(const KParams& P, int B, int S, const LaneWork& lw) {
+  const size_t waves = ((size_t)B * S + 63) / 64;
+  const size_t per_cu = (waves + 255) / 256;
+  const bool f64 = per_cu * seg_lds_bytes(P.N, S, false) <= 160 * 1024;
+  const bool f32 = per_cu * seg_lds_bytes(P.N, S, false, true) <= 160 * 1024;
+  if (lw.seg32 && f32) return 2;
+  return f64 ? 1 : (f32 ? 2 : 0);
+}
+
 template <int S, bool ROT>
 hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                              float* uo, float* xo, int* st, int* its, const WarmState& ws,
                              const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   constexpr int L = 64 / S;
   const int waves = (B + L - 1) / L;
+  const int mode = seg_scratch_mode(P, B, S, lw);
   // the lam-gains stored (FST, no refresh sweep: measured C5 30.5 -> see DESIGN.md 2b') when the
   // resident waves' LDS holds 14 doubles per stage, else the refresh sweep (11); lw.dref = 0
   // forces the refresh (test hook, F110QP_LANE_DREF=0)
   const size_t per_cu = ((size_t)waves + 255) / 256;
-  const bool fst = lw.dref && per_cu * seg_lds_bytes(P.N, S, true) <= 160 * 1024;
+  const bool fst = mode == 1 && lw.dref && per_cu * seg_lds_bytes(P.N, S, true) <= 160 * 1024;
   auto go = [&](auto kern, size_t lds) -> hipError_t {
     if (lds > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -747,6 +777,7 @@ hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const flo
                        lw.kmax, oo);
     return hipGetLastError();
   };
+  if (mode == 2) return go(&lane_seg_kernel<S, ROT, false, float>, seg_lds_bytes(P.N, S, false, true));
   return fst ? go(&lane_seg_kernel<S, ROT, true>, seg_lds_bytes(P.N, S, true))
              : go(&lane_seg_kernel<S, ROT, false>, seg_lds_bytes(P.N, S, false));
 }

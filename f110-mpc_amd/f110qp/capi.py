@@ -196,6 +196,39 @@ def _tp(t):
     return None if t is None else C.c_void_p(t.data_ptr())
 
 
+def _dev(t, dtype: str, n: int, name: str, optional: bool = False, where: bool = False):
+    """Check a device tensor before its raw pointer crosses the C ABI: a contiguous CUDA (HIP)
+    tensor of the ABI's element type with at least n elements (the kernels write / read exactly
+    that many; a float32 tensor where the ABI wants float64, or an int64 one where it wants int32,
+    would be an out-of-bounds write or a silent misread)."""
+    if t is None:
+        if optional:
+            return
+        raise F110QPError(f"{name} is required")
+    import torch
+
+    want = {"f32": torch.float32, "f64": torch.float64, "i32": torch.int32, "u8": torch.uint8}[dtype]
+    if not isinstance(t, torch.Tensor):
+        raise F110QPError(f"{name} must be a torch tensor on the device, got {type(t).__name__}")
+    if t.dtype != want:
+        raise F110QPError(f"{name} must be {want}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise F110QPError(f"{name} must be contiguous")
+    if t.numel() < n:
+        raise F110QPError(f"{name} holds {t.numel()} elements, the call needs {n}")
+    if where and t.device.type != "cuda":
+        raise F110QPError(f"{name} must be a device (cuda/HIP) tensor, got {t.device}")
+
+
+def _devs(*specs):
+    """_dev over several (tensor, dtype, n, name[, optional]) specs: every type / size check
+    first, then the placement of each (so a host-side test sees the type errors)."""
+    for sp in specs:
+        _dev(*sp)
+    for sp in specs:
+        _dev(*sp[:4], *(sp[4:] or (False,)), where=True)
+
+
 class Solver:
     """One f110qp context (device workspace). Mirrors the reference's OsqpEigen::Solver
     member of MPC (include/f110-mpc/mpc.h:63) for B instances at once."""
@@ -261,6 +294,22 @@ class Solver:
                                            _p(st), _p(it)), "f110qp_solve_batch")
         return u, x, st, it
 
+    def _check_dev(self, x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters=None, obj=None, cost=None,
+                   group=None):
+        """Shapes, element types and placement of a device call's tensors (see _dev)."""
+        B = int(x0.shape[0])
+        N = self.horizon
+        S = self.config.x_ref_points or N
+        specs = [(x0, "f32", 3 * B, "x0"), (u_lin, "f32", 2 * B, "u_lin"), (x_ref, "f32", 3 * S * B, "x_ref"),
+                 (halfspace, "f32", 6 * B, "halfspace", self.config.gap_mode == GAP_INACTIVE),
+                 (u_out, "f32", 2 * N * B, "u_out"), (x_out, "f32", 3 * (N + 1) * B, "x_out"),
+                 (status, "i32", B, "status"), (iters, "i32", B, "iters", True), (obj, "f64", B, "obj", True),
+                 (cost, "f64", B, "cost", True)]
+        if group is not None:
+            specs.append((group, "i32", B, "group"))
+        _devs(*specs)
+        return B
+
     def solve_dev(self, x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters=None, stream=None,
                   obj=None, cost=None):
         """Device (torch) tensors in/out, enqueued on `stream` (torch.cuda stream or None =
@@ -268,7 +317,7 @@ class Solver:
         (f110qp_solve_batch_ex_dev)."""
         import torch
 
-        B = x0.shape[0]
+        B = self._check_dev(x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters, obj, cost)
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
         if obj is not None or cost is not None:
@@ -287,6 +336,7 @@ class Solver:
         pays; bench.py's timed steps use it so Python argument marshalling is not the step)."""
         import torch
 
+        self._check_dev(x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters)
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
         fn = self.lib.f110qp_solve_batch_dev
@@ -304,6 +354,7 @@ class Solver:
         """prepare_dev for f110qp_solve_grouped_dev."""
         import torch
 
+        self._check_dev(x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters, group=group)
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
         fn = self.lib.f110qp_solve_grouped_dev
@@ -377,7 +428,7 @@ class Solver:
         optional float64 [B] (f110qp_solve_grouped_ex_dev)."""
         import torch
 
-        B = x0.shape[0]
+        B = self._check_dev(x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters, obj, cost, group=group)
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
         if obj is not None or cost is not None:
@@ -410,6 +461,9 @@ def select_dev(group, num_groups, cost, status, winner, best_cost, stream=None):
     status [B] i32 -> winner [G] i32 (-1: no solved candidate), best_cost [G] f64."""
     import torch
 
+    B = int(group.shape[0])
+    _devs((group, "i32", B, "group"), (cost, "f64", B, "cost"), (status, "i32", B, "status"),
+          (winner, "i32", int(num_groups), "winner"), (best_cost, "f64", int(num_groups), "best_cost"))
     if stream is None:
         stream = torch.cuda.current_stream(cost.device)
     _check(load().f110qp_select_dev(int(group.shape[0]), _tp(group), int(num_groups), _tp(cost), _tp(status),
@@ -443,6 +497,8 @@ def find_half_spaces_dev(states, ranges, angle_min, angle_inc, angle_max, hs_out
     if stream is None:
         stream = torch.cuda.current_stream(states.device)
     B, R = ranges.shape
+    _devs((states, "f32", 3 * B, "states"), (ranges, "f32", B * R, "ranges"), (hs_out, "f32", 6 * B, "hs_out"),
+          (gap_lo, "i32", B, "gap_lo", True), (gap_hi, "i32", B, "gap_hi", True))
     _check(L.f110qp_find_half_spaces_dev(B, _tp(states), _tp(ranges), R, float(angle_min), float(angle_inc),
                                          float(angle_max), float(thresh), float(divider), float(buffer),
                                          _tp(hs_out), _tp(gap_lo), _tp(gap_hi), C.c_void_p(stream.cuda_stream)),

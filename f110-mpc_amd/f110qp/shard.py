@@ -62,9 +62,14 @@ def select_sharded(best, winner, pg=None):
     holds, for ALL scenarios g (global ids), its local best cost best[g] (float64, +inf when it
     has no solved candidate of g) and the GLOBAL index winner[g] of that candidate (int, -1 none),
     e.g. from f110qp_select_dev on its shard plus the shard offset. Returns the global (best,
-    winner) on every rank: the minimal cost over all ranks, ties to the smallest global index,
-    i.e. exactly what one process selecting over the whole batch returns. Two all_reduce(MIN)
-    of G words each (RCCL over xGMI with the nccl backend: device tensors; gloo: host tensors)."""
+    winner) on every rank: the minimal cost over all ranks, ties to the smallest global index.
+    The min-loc is exact over the costs the ranks hold. Those equal the costs one process would
+    compute over the whole batch only when every rank's launch is the same kernel: the launch
+    policy depends on the per-rank batch size (lane_seg_kernel's S, lane vs wave back end), so
+    costs can differ in the last bits and a near-tie (candidates within rounding of each other)
+    may resolve to the other one; up to that it is what one process selecting over the whole
+    batch returns (tests/test_gpu_shard.py checks both cases). Two all_reduce(MIN) of G words
+    each (RCCL over xGMI with the nccl backend: device tensors; gloo: host tensors)."""
     import torch
     import torch.distributed as dist
 

@@ -84,6 +84,39 @@ def test_solve_argument_validation_without_gpu(capi):
     capi.Solver(capi.default_config(20)).close()  # create/destroy never touches the device
 
 
+def test_device_tensor_checks_before_the_abi(capi):
+    """The binding refuses tensors whose raw pointer would be misread or overrun by the kernels
+    (float32 obj/cost, int64 status/group/winner, short or strided buffers)."""
+    import torch
+
+    N, B = 20, 8
+    s = capi.Solver(capi.default_config(N))
+    f = lambda *sh: torch.zeros(*sh, dtype=torch.float32)  # noqa: E731
+    i = lambda *sh: torch.zeros(*sh, dtype=torch.int32)  # noqa: E731
+    args = [f(B, 3), f(B, 2), f(B, N, 3), None, f(B, N, 2), f(B, N + 1, 3), i(B)]
+    with pytest.raises(capi.F110QPError, match="obj must be torch.float64"):
+        s.solve_dev(*args, obj=f(B))
+    with pytest.raises(capi.F110QPError, match="status must be torch.int32"):
+        s.solve_dev(*args[:6], torch.zeros(B, dtype=torch.int64))
+    with pytest.raises(capi.F110QPError, match="u_out holds"):
+        s.solve_dev(*args[:4], f(B - 1, N, 2), *args[5:])
+    with pytest.raises(capi.F110QPError, match="x_ref must be contiguous"):
+        s.solve_dev(args[0], args[1], f(B, 3, N).transpose(1, 2), *args[3:])
+    with pytest.raises(capi.F110QPError, match="device"):
+        s.solve_dev(*args)  # host tensors
+    with pytest.raises(capi.F110QPError, match="group must be torch.int32"):
+        s.prepare_grouped_dev(*args[:4], torch.zeros(B, dtype=torch.int64), 2, *args[4:])
+    with pytest.raises(capi.F110QPError, match="best_cost must be torch.float64"):
+        capi.select_dev(i(B), 2, torch.zeros(B, dtype=torch.float64), i(B), i(2), f(2))
+    with pytest.raises(capi.F110QPError, match="winner holds"):
+        capi.select_dev(i(B), 4, torch.zeros(B, dtype=torch.float64), i(B), i(2), torch.zeros(4, dtype=torch.float64))
+    g = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE))
+    with pytest.raises(capi.F110QPError, match="halfspace is required"):
+        g.solve_dev(*args)
+    s.close()
+    g.close()
+
+
 def test_find_half_spaces_no_gap_is_an_error(capi):
     r = np.full(1080, 1.0, np.float32)
     with pytest.raises(capi.F110QPError, match="no gap"):
@@ -139,7 +172,8 @@ def test_qp_dims_match_reference_sizes(capi, oracle):
 
 def test_backend_info_resolves_auto_and_scratch(capi):
     """f110qp_backend_info (host only, no device needed): AUTO resolves to the lane back end at
-    the measured thresholds (F110QP_LANE_MIN_BATCH[_WIDE]), gap rows always to the wave back end;
+    the measured thresholds (F110QP_LANE_MIN_BATCH[_WIDE]), gap rows always to the wave back end
+    (an explicit F110QP_BACKEND_LANE runs the interior point where it fits);
     the lane QPs-per-wave fill <= 256 waves; the scratch sits in LDS (fp64 when it fits) while the
     grid's waves are resident with it and in HBM (fp32) at the C4 size."""
     s20 = capi.Solver(capi.default_config(20))
@@ -157,11 +191,21 @@ def test_backend_info_resolves_auto_and_scratch(capi):
     # horizons S does not divide: segments of floor(N / S) or one more stage (the reference's
     # default N = 30 and odd N)
     s30, s25 = capi.Solver(capi.default_config(30)), capi.Solver(capi.default_config(25))
-    assert s30.lane_segments(4096) == 8 and s25.lane_segments(4096) == 8 and s30.lane_segments(16384) == 1  # S = 2 would need 222 KB of LDS per CU
+    assert s30.lane_segments(4096) == 8 and s25.lane_segments(4096) == 8
+    # fp64 scratch at 16,384 x N = 30 would need 222 KB of LDS per CU: float scratch, S = 4
+    assert s30.lane_segments(16384) == 4 and s30.backend_info(16384)[2] == 2
+    # the middle of the C4 curve (65,536 over 4 / 2 GPUs): 16,384 x N = 40 on fp32 LDS scratch at
+    # S = 4; 32,768 does not fit four waves per CU and keeps the HBM-scratch sequential kernel
+    assert s40.lane_segments(16384) == 4 and s40.backend_info(16384) == (capi.BACKEND_LANE, 16, 2)
+    assert s40.lane_segments(32768) == 1 and s40.backend_info(32768)[2] == 4
     s30.close()
     s25.close()
     assert s40.backend_info(65536, grouped=True) == (capi.BACKEND_LANE, 64, 4)
     sg = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE))
-    assert sg.backend_info(65536)[0] == capi.BACKEND_WAVE
+    assert sg.backend_info(65536)[0] == capi.BACKEND_WAVE and sg.backend_info(4096)[0] == capi.BACKEND_WAVE
+    sl = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE, backend=capi.BACKEND_LANE))
+    assert sl.backend_info(4096) == (capi.BACKEND_LANE, 16, 1) and sl.lane_segments(4096) == 4
+    assert sl.backend_info(65536)[0] == capi.BACKEND_WAVE  # the interior point's LDS does not fit
+    sl.close()
     for s in (s20, s40, sg):
         s.close()

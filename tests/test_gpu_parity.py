@@ -433,6 +433,26 @@ def test_c4_grouped_candidates_horizon40(oracle, capi):
     assert rel_err(u[idx], ur).max() <= TOL and rel_err(x[idx], xr).max() <= TOL
 
 
+def test_c4_full_single_gpu_batch(oracle, capi):
+    """BASELINE configs[3] at its full single-GPU size: 65,536 x N = 40 grouped candidates (546
+    scenarios x 120 + 16), the launch the c4 bench line times (AUTO: lane_kernel with fp32
+    Riccati-gain scratch in HBM). Every QP solved; parity on a strided sample of 1,024 QPs plus
+    every candidate of one whole scenario."""
+    N, B = 40, 65536
+    g = workload.make_grouped_batch(-(-B // 120), N, seed=4000)
+    w = {k: np.ascontiguousarray(g[k][:B]) for k in ("x0", "u_lin", "x_ref")}
+    s = capi.Solver(capi.default_config(N))
+    be, qpw, scr = s.backend_info(B)
+    assert be == capi.BACKEND_LANE and s.lane_segments(B) == 1 and scr == 4  # HBM fp32
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    assert (st == capi.SOLVED).all()
+    idx = np.concatenate([np.arange(0, B, 64), np.arange(32760, 32880)])
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
+    assert (sr == oracle.SOLVED).all()
+    assert rel_err(u[idx], ur).max() <= 2e-6 and rel_err(x[idx], xr).max() <= 2e-6
+
+
 def test_warm_started_stream_horizon40(oracle, capi):
     """warm_start at N = 40: the act masks of both register rows carry across ticks."""
     N, B, T = 40, 256, 4
@@ -608,10 +628,13 @@ def test_lane_backend_scratch_modes(oracle, capi, monkeypatch, mode):
     HBM fp32, F110QP_LANE_MODE) gives the exact optimum within the tolerance; N = 40 covers
     the fall-back of LDS fp64 (too big) to HBM."""
     monkeypatch.setenv("F110QP_LANE_MODE", mode)
+    lo, hi = np.float32([3.0, -0.43]), np.float32([4.5, 0.43])
     for N, seed in ((20, 811), (40, 812)):
         w = workload.make_batch(1500, N, seed=seed, heading="true", lateral=1.2, steer_range=0.8)
         u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE, tol=2e-6)
         assert (st == capi.SOLVED).all()
+        # fp32 gains: the output clamps an input the single-flip tolerance left outside its box
+        assert (u >= lo).all() and (u <= hi).all()
 
 
 

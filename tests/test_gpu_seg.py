@@ -185,3 +185,52 @@ def test_segments_refresh_and_stored_gains_agree(oracle, capi, monkeypatch, S, N
         out[dref] = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
     np.testing.assert_array_equal(out["0"][2], out["1"][2])
     assert rel_err(out["1"][0], out["0"][0].astype(np.float64)).max() <= 1e-6
+
+
+@pytest.mark.parametrize("S,N", [(2, 20), (4, 20), (8, 40), (4, 40), (2, 40), (4, 30)])
+def test_segments_fp32_scratch(oracle, capi, monkeypatch, S, N):
+    """Float references and Riccati scratch (F110QP_LANE_SEG_F32=1; AUTO takes them where fp64
+    does not fit, e.g. 16,384 x N = 40): many active bounds on both faces, the exact optimum within
+    the fp32-gain tolerance of test_lane_backend_scratch_modes."""
+    monkeypatch.setenv("F110QP_LANE_SEG", str(S))
+    monkeypatch.setenv("F110QP_LANE_SEG_F32", "1")
+    w = workload.make_batch(1000, N, seed=9300 + 10 * S + N, heading="true", lateral=1.5, steer_range=1.0)
+    s = _lane(capi, N)
+    assert s.lane_segments(1000) == S
+    assert s.backend_info(1000)[2] == 2  # LDS fp32
+    s.close()
+    u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE, tol=2e-6)
+    assert (st == capi.SOLVED).all()
+    assert (u >= np.float32([3.0, -0.43])).all() and (u <= np.float32([4.5, 0.43])).all()
+
+
+@pytest.mark.parametrize("kmax", ["16", "0"])
+def test_segments_fp32_degenerate_bound(oracle, capi, monkeypatch, kmax):
+    """des_vel = umax with Q = 0 / tiny Q (a zero-multiplier active bound) on fp32 scratch: the
+    single-flip passes' fp32 tolerance settles it (lane_kernel.h's HBM-fp32 rule)."""
+    monkeypatch.setenv("F110QP_LANE_SEG", "4")
+    monkeypatch.setenv("F110QP_LANE_SEG_F32", "1")
+    monkeypatch.setenv("F110QP_LANE_KMAX", kmax)
+    N = 20
+    for q in ([0.0, 0.0, 0.0], [1e-9, 1e-9, 0.0], [1e-3, 1e-3, 0.0]):
+        w = workload.make_batch(700, N, seed=4500, heading="true", lateral=0.0, steer_range=0.0)
+        u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE, tol=1e-5, q=q)
+        assert (st == capi.SOLVED).all(), (q, np.unique(st, return_counts=True))
+
+
+def test_c4_16384_per_gpu_auto(oracle, capi):
+    """The middle of the C4 strong-scaling curve: 16,384 x N = 40 QPs per GPU (65,536 over 4
+    GPUs). AUTO runs the segmented kernel at S = 4 on fp32 scratch (fp64 does not fit four waves
+    per CU); parity on a strided sample plus two whole scenarios."""
+    N, B = 40, 16384
+    g = workload.make_grouped_batch(137, N, seed=4043)
+    w = {k: np.ascontiguousarray(g[k][:B]) for k in ("x0", "u_lin", "x_ref")}
+    s = capi.Solver(capi.default_config(N))
+    assert s.lane_segments(B) == 4 and s.backend_info(B)[2] == 2
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    assert (st == capi.SOLVED).all()
+    idx = np.concatenate([np.arange(0, B, 23), np.arange(600, 840)])
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
+    assert (sr == oracle.SOLVED).all()
+    assert rel_err(u[idx], ur).max() <= 2e-6 and rel_err(x[idx], xr).max() <= 2e-6
