@@ -243,13 +243,33 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
     c1.warm_start = 0  # a cold solve per call: the latency of one control tick
     c1.x_ref_points = 0
     s1 = capi.Solver(c1)
-    dev_t, host_t, batch_t = [], [], []
+    dev_t, prep_t, host_t, batch_t = [], [], [], []
     for i in range(reps + 20):
         t0 = time.perf_counter()
         s1.solve_dev(one["x0"], one["u_lin"], one["x_ref"], h1, uo, xo, st, stream=stream)
         stream.synchronize()
         if i >= 20:
             dev_t.append(time.perf_counter() - t0)
+    # the same through the prepared launcher: one C call per tick (what a C++ caller of the ABI
+    # pays), no ctypes argument conversion
+    launch1 = s1.prepare_dev(one["x0"], one["u_lin"], one["x_ref"], h1, uo, xo, st, stream=stream)
+    for i in range(reps + 20):
+        t0 = time.perf_counter()
+        launch1()
+        stream.synchronize()
+        if i >= 20:
+            prep_t.append(time.perf_counter() - t0)
+    # the B = 1 kernel alone (HIP events over back-to-back launches)
+    ea = torch.cuda.Event(enable_timing=True)
+    eb = torch.cuda.Event(enable_timing=True)
+    ea.record(stream)
+    for _ in range(50):
+        launch1()
+    eb.record(stream)
+    torch.cuda.synchronize(dev)
+    k1_us = ea.elapsed_time(eb) * 1000.0 / 50
+    be1, _, _ = s1.backend_info(1)
+    seg1 = s1.lane_segments(1) if be1 == capi.BACKEND_LANE else 1
     hx = {k: np.ascontiguousarray(w[k][:1]) for k in ("x0", "u_lin", "x_ref")}
     hh = None if hs is None else hs[:1].cpu().numpy()
     for i in range(reps + 20):
@@ -264,9 +284,13 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
         stream.synchronize()
         if i >= 5:
             batch_t.append(time.perf_counter() - t0)
-    return {"single_qp_device": pct(dev_t), "single_qp_host_pointers": pct(host_t),
-            "batch_launch": pct(batch_t),
-            "note": "wall clock per call incl. launch + stream sync; host-pointer path adds H2D/D2H over PCIe"}
+    return {"single_qp_device": pct(prep_t), "single_qp_device_ctypes": pct(dev_t),
+            "single_qp_host_pointers": pct(host_t), "batch_launch": pct(batch_t),
+            "single_qp_kernel_us": k1_us,
+            "single_qp_backend": ("lane" + (f" (S = {seg1})" if seg1 > 1 else "")) if be1 == capi.BACKEND_LANE else "wave",
+            "note": "wall clock per call incl. launch + stream sync: single_qp_device through the prepared "
+                    "launcher (one C call), _ctypes with the per-call argument conversion; host-pointer path "
+                    "adds H2D/D2H over PCIe"}
 
 
 def _halfspaces_host(w, B):

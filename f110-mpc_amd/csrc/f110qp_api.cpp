@@ -316,16 +316,17 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   lw->ipm = c->ipm;
   *backend = resolve_backend(c, batch, grouped, *lw) == F110QP_BACKEND_LANE ? f110qp::BACKEND_LANE
                                                                            : f110qp::BACKEND_WAVE;
-  if (*backend == f110qp::BACKEND_WAVE) return F110QP_OK;
   (void)s;
   hipError_t e;
   if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) {
-    // hand-over count + list of the interior-point kernel
+    // count + list of the interior point's hand-over (lane back end) or of the fp64 re-check of
+    // the wave kernel's non-SOLVED QPs (wave back end)
     if ((e = c->hand.ensure(((size_t)batch + 1) * sizeof(int))) != hipSuccess)
       return hip_fail(e, "hipMalloc hand-over list");
     lw->hand = (int*)c->hand.p;
     return F110QP_OK;
   }
+  if (*backend == f110qp::BACKEND_WAVE) return F110QP_OK;
   // HBM scratch of ceil(B/L) waves x N stages x 8 values x L lanes (<= (B + 63) x N x 8 doubles)
   const size_t N = (size_t)c->cfg.horizon;
   e = c->lscr.ensure(((size_t)batch + 63) * N * 8 * sizeof(double));

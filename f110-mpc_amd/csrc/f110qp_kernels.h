@@ -102,6 +102,14 @@ hipError_t launch_lane_ipm(const KParams& P, int B, const float* x0, const float
                            int* status, int* iters, const LaneWork& lw, const ObjOut& oo,
                            hipStream_t stream);
 
+// fp64 re-check of the wave kernel's gap-row QPs it did not report SOLVED (lane_ipm_inst.hip):
+// the interior point over their list; polished -> SOLVED, Farkas certificate -> PRIMAL_INFEASIBLE,
+// else the wave kernel's answer stands. Needs lw.hand (B + 1 ints).
+hipError_t launch_gap_recheck(const KParams& P, int B, const float* x0, const float* u_lin,
+                              const float* x_ref, const float* hs, float* u_out, float* x_out,
+                              int* status, int* iters, const LaneWork& lw, const ObjOut& oo,
+                              hipStream_t stream);
+
 enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
 
 // Solve B QPs. hs == nullptr -> box-only kernels (gap rows inactive). backend LANE: box rows, the

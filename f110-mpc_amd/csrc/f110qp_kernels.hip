@@ -52,9 +52,12 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
     return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 1,
                           lw.hand, B < kHandGrid ? B : kHandGrid, oo, s);
   }
-  if (hs)
-    return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
-                          nullptr, B, oo, s);
+  if (hs) {
+    hipError_t e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
+                                  nullptr, B, oo, s);
+    if (e != hipSuccess) return e;
+    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s);
+  }
   if (backend == BACKEND_LANE) return launch_lane(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
   return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
                          nullptr, B, oo, s);
@@ -98,10 +101,12 @@ hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const 
   e = hs ? launch_prep_g<true>(P, B, x0, ul, xr, hs, gws, leader, s)
          : launch_prep_g<false>(P, B, x0, ul, xr, hs, gws, leader, s);
   if (e != hipSuccess) return e;
-  return hs ? launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, gws, nullptr,
-                             nullptr, B, oo, s)
-            : launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, gws,
-                              nullptr, nullptr, B, oo, s);
+  if (hs) {
+    e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, gws, nullptr, nullptr, B, oo, s);
+    if (e != hipSuccess) return e;
+    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s);
+  }
+  return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, gws, nullptr, nullptr, B, oo, s);
 }
 
 hipError_t launch_condense_debug(const KParams& P, int B, const float* x0, const float* ul,

@@ -90,19 +90,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_IPM_W
     const KParams P, const int B, const float* __restrict__ x0g, const float* __restrict__ ulg,
     const float* __restrict__ xrg, const float* __restrict__ hsg, float* __restrict__ uout,
     float* __restrict__ xout, int* __restrict__ status_out, int* __restrict__ iters_out,
-    int* __restrict__ hand_list, int* __restrict__ hand_count, const IpmKnobs kn, const ObjOut oo) {
+    int* __restrict__ hand_list, int* __restrict__ hand_count, const IpmKnobs kn, const ObjOut oo,
+    const int* __restrict__ qlist, const int* __restrict__ qcount, const int recheck) {
   constexpr int L = 64 / S;  // QPs per wave
   constexpr int NF = kIpmNF;
   extern __shared__ __attribute__((aligned(16))) double ipm_smem[];
   const int lane = threadIdx.x;
   const int sl = lane & (L - 1);
   const int seg = lane / L;
+  // list mode (qlist): the wave takes list items b0 .. b0 + L - 1 of the device list (the wave
+  // kernel's flagged QPs); otherwise QPs b0 .. b0 + L - 1 of the batch
+  const int nb = qlist ? __builtin_amdgcn_readfirstlane(*qcount) : B;
   const int b0 = blockIdx.x * L;
-  const int nq = (B - b0) < L ? (B - b0) : L;
+  if (b0 >= nb) return;  // wave-uniform: an empty part of the list
+  const int nq = (nb - b0) < L ? (nb - b0) : L;
   const int slot = sl < nq ? sl : 0;  // a missing QP's lanes duplicate QP 0 of the wave
   const bool owner = sl < nq;
   const bool qowner = owner && seg == 0;
-  const int b = b0 + slot;
+  const int b = qlist ? qlist[b0 + slot] : b0 + slot;
   const int N = P.N;
   const int q = N / S, rem = N - q * S;
   const int m = q + (seg < rem ? 1 : 0);
@@ -125,11 +130,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_IPM_W
   {
     float* stg = reinterpret_cast<float*>(ipm_smem + 3 * mM * 64);
     const int n3 = 3 * N, S3 = 3 * P.xr_stride, tot = nq * n3;
-    const float* src = xrg + (size_t)b0 * S3;
+    const float* src = xrg + (qlist ? (size_t)0 : (size_t)b0 * S3);
     const int dq = 64 / n3, dc = 64 - dq * n3;
     int qq = lane / n3, c = lane - (lane / n3) * n3;
     const int junk = n3 * L + lane;
-    const int last_off = (nq - 1) * S3 + (n3 - 1);
+    const size_t last_off = (size_t)(qlist ? qlist[b0 + nq - 1] : nq - 1) * S3 + (n3 - 1);
     constexpr int kChunk = 16;
     for (int e0 = 0; e0 < tot; e0 += kChunk * 64) {
       float vbuf[kChunk];
@@ -138,7 +143,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_IPM_W
       for (int j = 0; j < kChunk; j++) {
         const bool in = e0 + j * 64 + lane < tot;
         dst[j] = in ? c * L + qq : junk;
-        vbuf[j] = src[in ? qq * S3 + c : last_off];
+        vbuf[j] = src[in ? (size_t)(qlist ? qlist[b0 + qq] : qq) * S3 + c : last_off];
         qq += dq;
         c += dc;
         const bool wrap = c >= n3;
@@ -785,13 +790,78 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_IPM_W
     step_stage(t, u0, u1, x0, x1, x2, sv, zv);
   }
 
-  // ---- outputs: the polished point (fp64) in the reference frame ----
   const bool solved = (done && !bad && !handover0 && iters > 0) || (kn.debug && !bad);
-  const bool hand = !bad && !solved;
+
+  // ---- infeasibility certificate (Farkas) for the QPs the interior point did not polish ----
+  // On an empty feasible set the multipliers of the gap rows grow without bound; y = z_gap /
+  // max z_gap then nearly annihilates the reachable set. For ANY y >= 0 the bound
+  //   max_{u in box} y'c_gap(x(u)) = y'c_gap(u_k) + sum_i sum_a [max(g_ia lb_a, g_ia ub_a) - g_ia u_ia],
+  //   g_i = B' G_{i+1},  G_{i+1} = sum_k y_ik nu_k + A' G_{i+2}  (the costate of y'c_gap, dynamics
+  //   model.cpp:42-51, rows mpc.cpp:249,271)
+  // is exact (c_gap is affine in u); a negative value proves that no input in the box satisfies
+  // every gap row: PRIMAL_INFEASIBLE, as OSQP reports it. Checked in fp64 on every QP still open.
+  bool infeas = false;
+  {
+    const bool open_qp = !solved && !bad && !handover0;
+    if (__ballot(open_qp) != 0ull) {
+      double ym = 0.0;
+      for (int t = 0; t < m; t++) ym = fmax(ym, fmax(F(t, kFZ + 4), F(t, kFZ + 5)));
+#pragma unroll
+      for (int k = L; k < 64; k <<= 1) ym = fmax(ym, __shfl_xor(ym, k, 64));
+      const double iy = ym > 0.0 ? 1.0 / ym : 0.0;
+      // the segment's own contribution to the costate at its start (incoming G = 0)
+      double G0 = 0.0, G1 = 0.0, G2 = 0.0, val = 0.0;
+      for (int t = m - 1; t >= 0; t--) {
+        const double y0 = F(t, kFZ + 4) * iy, y1 = F(t, kFZ + 5) * iy;
+        const double xn0 = F(t, kFXn), xn1 = F(t, kFXn + 1);
+        val += y0 * (n0s * xn0 + n0n * xn1 - be0) + y1 * (n1s * xn0 + n1n * xn1 - be1);
+        G0 += y0 * n0s + y1 * n1s;
+        G1 += y0 * n0n + y1 * n1n;
+        G2 = ROT ? G2 + a12 * G1 : G2 + a02 * G0 + a12 * G1;  // A' G
+      }
+      // incoming costate from the segments above: G_in(j) = (A')^m_{j+1} G_in(j+1) + local(j+1)
+      double gi0 = 0.0, gi1 = 0.0, gi2 = 0.0;
+      if constexpr (S > 1) {
+        const double md = (double)m;
+#pragma unroll 1
+        for (int it2 = 0; it2 < S - 1; it2++) {
+          const double o0 = gi0 + G0, o1 = gi1 + G1;
+          const double o2 = gi2 + (ROT ? md * a12 * gi1 : md * (a02 * gi0 + a12 * gi1)) + G2;
+          const double r0_ = __shfl(o0, up), r1_ = __shfl(o1, up), r2_ = __shfl(o2, up);
+          gi0 = top ? 0.0 : r0_;
+          gi1 = top ? 0.0 : r1_;
+          gi2 = top ? 0.0 : r2_;
+        }
+      }
+      // g_i = B' G_{i+1} with the incoming costate, and the box maximum of each input term
+      double box = 0.0;
+      {
+        double c0_ = gi0, c1_ = gi1, c2_ = gi2;
+        for (int t = m - 1; t >= 0; t--) {
+          const double y0 = F(t, kFZ + 4) * iy, y1 = F(t, kFZ + 5) * iy;
+          c0_ += y0 * n0s + y1 * n1s;
+          c1_ += y0 * n0n + y1 * n1n;
+          const double g0 = ROT ? b00 * c0_ + b20 * c2_ : b00 * c0_ + b10 * c1_ + b20 * c2_;
+          const double g1 = b21 * c2_;
+          const double u0 = F(t, kFU), u1 = F(t, kFU + 1);
+          box += fmax(g0 * lb0, g0 * ub0) - g0 * u0 + fmax(g1 * lb1, g1 * ub1) - g1 * u1;
+          c2_ = ROT ? c2_ + a12 * c1_ : c2_ + a02 * c0_ + a12 * c1_;
+        }
+      }
+      const double cert = qsum(val + box);
+      infeas = open_qp && ym > 0.0 && cert < -1e-9;
+    }
+  }
+
+  // ---- outputs: the polished point (fp64) in the reference frame ----
+  // hand-over: open QPs without a certificate go to the wave kernel's GI (normal mode); in the
+  // re-check mode (the wave kernel's flagged QPs) only a polished or certified answer is written
+  const bool hand = !bad && !solved && !infeas && !recheck;
+  const bool wr = recheck ? (solved || infeas) : !hand;
   const float nanv = __int_as_float(0x7fc00000);
   float* uo = uout + (size_t)b * 2 * N;
   float* xo = xout + (size_t)b * 3 * (N + 1);
-  if (qowner && !hand) {
+  if (qowner && wr) {
     xo[0] = solved ? fX0 : nanv;
     xo[1] = solved ? fY0 : nanv;
     xo[2] = solved ? fTH0 : nanv;
@@ -815,7 +885,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_IPM_W
         J += 0.5 * (r0 * (u0 - ud0) * (u0 - ud0) + r1 * (u1 - ud1) * (u1 - ud1));
       }
       x0 = F(t, kFXn); x1 = F(t, kFXn + 1); x2 = F(t, kFXn + 2);
-      if (owner && !hand) {
+      if (owner && wr) {
         uo[2 * i] = solved ? (float)u0 : nanv;
         uo[2 * i + 1] = solved ? (float)u1 : nanv;
         const double ox = ROT ? cs * x0 - sn * x1 : x0, oy = ROT ? sn * x0 + cs * x1 : x1;
@@ -831,24 +901,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_IPM_W
     Cr = qsum(Cr);
     const double Cu = 0.5 * (double)N * (r0 * ud0 * ud0 + r1 * ud1 * ud1);
     const double dnan = __longlong_as_double(0x7ff8000000000000ll);
-    if (qowner && !hand && oo.cost) oo.cost[b] = solved ? J : dnan;
-    if (qowner && !hand && oo.obj) oo.obj[b] = solved ? J - Cr - Cu : dnan;
+    if (qowner && wr && oo.cost) oo.cost[b] = solved ? J : dnan;
+    if (qowner && wr && oo.obj) oo.obj[b] = solved ? J - Cr - Cu : dnan;
   }
   if (qowner) {
     if (hand) {
       const int idx = atomicAdd(hand_count, 1);
       hand_list[idx] = b;
-    } else {
-      status_out[b] = bad ? F110QP_NUMERICAL_ID : F110QP_SOLVED_ID;
-      if (iters_out) iters_out[b] = bad ? 0 : iters;
+    } else if (wr) {
+      status_out[b] = bad ? F110QP_NUMERICAL_ID : (solved ? F110QP_SOLVED_ID : F110QP_PRIMAL_INFEASIBLE_ID);
+      if (iters_out) iters_out[b] = bad ? 0 : (solved ? iters : kn.max_iter);
     }
+  }
+}
+
+// The wave kernel's QPs with gap rows that it did not certify (SOLVED_INACCURATE, MAX_ITER) or
+// declared infeasible / numerically broken: the list the interior point re-checks in fp64.
+__global__ __launch_bounds__(256) void ipm_flag_kernel(const int B, const int* __restrict__ status,
+                                                      int* __restrict__ count, int* __restrict__ list) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b < B) {
+    const int s = status[b];
+    if (s != F110QP_SOLVED_ID) list[atomicAdd(count, 1)] = b;
   }
 }
 
 template <int S, bool ROT>
 hipError_t launch_lane_ipm_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                              const float* hs, float* uo, float* xo, int* st, int* its, int* list, int* count,
-                             const IpmKnobs& kn, const ObjOut& oo, hipStream_t s) {
+                             const IpmKnobs& kn, const ObjOut& oo, hipStream_t s, const int* qlist = nullptr,
+                             const int* qcount = nullptr, int recheck = 0) {
   constexpr int L = 64 / S;
   const int waves = (B + L - 1) / L;
   const size_t lds = ipm_lds_bytes(P.N, S);
@@ -859,7 +941,7 @@ hipError_t launch_lane_ipm_t(const KParams& P, int B, const float* x0, const flo
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(kern, dim3(waves), dim3(64), lds, s, P, B, x0, ul, xr, hs, uo, xo, st, its, list,
-                     count, kn, oo);
+                     count, kn, oo, qlist, qcount, recheck);
   return hipGetLastError();
 }
 

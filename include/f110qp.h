@@ -47,7 +47,8 @@
  *                            with different references are compared on `cost`: obj carries the
  *                            reference-dependent constant -1/2 sum x_ref'Q x_ref.
  *    On a non-SOLVED status u_out/x_out hold NaN (obj/cost too), as OSQP's solution does on
- *    failure.
+ *    failure, with one exception: F110QP_SOLVED_INACCURATE returns the finite but uncertified
+ *    point (u, x, obj, cost written; see the status below).
  */
 #ifndef F110QP_H
 #define F110QP_H
@@ -66,8 +67,12 @@ extern "C" {
 
 /* per-QP status codes (values follow OSQP's status ids) */
 #define F110QP_SOLVED 1
-#define F110QP_SOLVED_INACCURATE 2 /* wave back end: a point whose fp64 KKT check failed (u, x    */
-                                  /* written, not selected); see DESIGN.md, stiff problems     */
+#define F110QP_SOLVED_INACCURATE 2 /* wave back end: a point whose fp64 KKT check failed and    */
+                                  /* that the fp64 re-check (gap rows: the lane interior point)  */
+                                  /* could not certify either: u, x, obj, cost are written but   */
+                                  /* not certified, and f110qp_select_dev never picks it. Its    */
+                                  /* active set may seed the next warm start (a seed is only a   */
+                                  /* first guess; every solve is certified on its own).          */
 #define F110QP_MAX_ITER -2
 #define F110QP_PRIMAL_INFEASIBLE -3
 #define F110QP_NUMERICAL -10      /* non-finite data or factorisation breakdown */
@@ -80,9 +85,14 @@ extern "C" {
 #define F110QP_BACKEND_AUTO 0     /* lane-per-QP for box-only batches >= F110QP_LANE_MIN_BATCH  */
                                   /* (N <= 32) or >= F110QP_LANE_MIN_BATCH_WIDE (N > 32)       */
 #define F110QP_BACKEND_WAVE 1     /* one wavefront per QP: condensed W = H^-1 + PDAS/GI         */
-#define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64 (box rows only;      */
-                                  /* gap rows always use the wave back end)                    */
-/* AUTO thresholds, measured on MI355X (kernel us, DESIGN.md section 6, round 3: the lane back end
+#define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64; with gap rows the   */
+                                  /* Riccati interior point (lane_ipm_kernel.h) where its LDS  */
+                                  /* fits (else the wave back end); QPs it does not polish go  */
+                                  /* to the wave kernel's GI in the same call                  */
+/* Gap rows: AUTO keeps the wave back end (C3, 4,096 x N = 20: wave GI 290 us, lane interior point
+ * 1,010 us); the wave kernel's gap-row QPs it does not report SOLVED are re-checked
+ * in fp64 by the interior point in the same call (KKT-checked polish or a Farkas certificate).
+ * AUTO thresholds, measured on MI355X (kernel us, DESIGN.md section 6, round 3: the lane back end
  * with the partitioned-horizon kernel below one wave per SIMD, the wave back end with its fp64
  * certification). N = 20 (C2 recipe, cold): wave 27.3 vs lane 30.6 at 512 (before the last
  * segmented-kernel changes), 28.5 vs 27.7 at 1,024, 53.1 vs 36.3 at 2,048, 93.0 vs 37.0 at
@@ -201,13 +211,15 @@ int f110qp_select_dev(int batch, const int* group, int num_groups, const double*
 /* The launch a solve call of `batch` QPs on this context makes (grouped != 0: the grouped entry
  * points): backend = F110QP_BACKEND_WAVE or _LANE (what AUTO resolves to), qps_per_wave (lane:
  * QPs per 64-lane wavefront; wave: 1) and scratch (lane: 1 LDS fp64, 2 LDS fp32, 3 HBM fp64,
- * 4 HBM fp32 Riccati gain scratch; wave: 0). Any pointer may be NULL. */
+ * 4 HBM fp32 Riccati gain scratch; the partitioned-horizon kernel uses 1 or 2 (float references
+ * and scratch where fp64 does not fit), the interior point 1; wave: 0). Any pointer may be NULL. */
 int f110qp_backend_info(f110qp_ctx* ctx, int batch, int grouped, int* backend, int* qps_per_wave,
                         int* scratch);
 
 /* Horizon segments per QP of that launch: 1, or S = 2 / 4 / 8 when the lane back end splits each
  * QP's horizon over S lanes (partitioned Riccati; batches too small to give every SIMD a wave of
- * distinct QPs). The result is the exact optimum either way. */
+ * distinct QPs; with gap rows on the lane back end the interior point's S = 2..16).
+ * The result is the exact optimum either way. */
 int f110qp_lane_segments(f110qp_ctx* ctx, int batch, int* segments);
 
 /* Forget the warm-start state of every slot (the next call solves cold). */
