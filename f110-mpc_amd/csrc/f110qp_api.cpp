@@ -297,7 +297,8 @@ static int resolve_backend(f110qp_ctx* c, int batch, bool grouped, const f110qp:
     const int min_b = grouped ? (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH_GROUPED
                                                       : F110QP_LANE_MIN_BATCH_GROUPED_WIDE)
                               : (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH : F110QP_LANE_MIN_BATCH_WIDE);
-    be = batch >= min_b ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
+    const bool small = !grouped && c->cfg.horizon <= 32 && batch <= F110QP_LANE_MAX_SMALL_BATCH;
+    be = (batch >= min_b || small) ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
   }
   return be;
 }

@@ -24,28 +24,43 @@ constexpr size_t seg_lds_per_wave(int N, int S, bool f32 = false) {
 // Horizon segments per QP (lane_seg_kernel.h). A batch whose waves leave SIMDs idle (the QPs fit
 // in fewer than one wave per SIMD at 64 / S QPs per wave) splits every QP's horizon over S lanes
 // instead of running 64 / L identical copies of it. S cuts N into segments of >= 2 stages (of
-// floor(N / S) or one more), the grid stays within one wave per SIMD (1,024 waves) and the
-// segmented LDS fits (fp64 references and scratch, or float ones where fp64 does not fit:
-// 16,384 x N = 40 runs S = 4 on fp32 scratch, round 4). Among those the launch takes the S with the shortest per-pass chain by the
+// floor(N / S) or one more), the grid stays within two waves per SIMD (2,048 waves) and a wave's
+// segmented LDS fits the CU (fp64 references and scratch when the whole grid is resident with
+// them, else float ones, possibly in more than one dispatch round: 16,384 x N = 40 runs S = 4 on
+// fp32 scratch in one round, 32,768 x N = 40 in two, round 4). Among those the launch takes the S with the shortest per-pass chain by the
 // instruction model of DESIGN.md 2b': sequential N x ~255 instructions, segmented ceil(N / S) x
 // ~350 + (S - 1) x ~230 (the two segment recursions). A forced QPs-per-wave or scratch placement
 // keeps lane_kernel.h.
 int lane_segments(const KParams& P, int B, const LaneWork& lw) {
   const int N = P.N;
-  auto fits = [&](int S) {
-    if (N / S < 2) return false;
+  // dispatch rounds of the segmented grid: waves per CU over the waves the CU's 160 KiB of LDS
+  // holds at once (fp64 scratch when the whole grid is resident with it, else float); 0 = no fit
+  // the cost multiplier is rounds x resident waves per SIMD (a second wave on a SIMD shares its
+  // fp64 issue slots: the kernels are VALU-issue bound)
+  auto rounds = [&](int S) -> int {
+    if (N / S < 2) return 0;
     const size_t waves = ((size_t)B * S + 63) / 64;
     const size_t per_cu = (waves + 255) / 256;
-    return per_cu <= 4 && per_cu * seg_lds_per_wave(N, S, true) <= 160 * 1024;
+    if (per_cu > 8) return 0;
+    size_t resident = per_cu;
+    if (per_cu * seg_lds_per_wave(N, S) > 160 * 1024) {
+      resident = (160 * 1024) / seg_lds_per_wave(N, S, true);
+      if (resident < 1) return 0;
+      if (resident > per_cu) resident = per_cu;
+    }
+    const size_t r = (per_cu + resident - 1) / resident;
+    return (int)(r * ((resident + 3) / 4));
   };
   if (lw.seg == 1) return 1;
-  if (lw.seg == 2 || lw.seg == 4 || lw.seg == 8) return fits(lw.seg) ? lw.seg : 1;
+  if (lw.seg == 2 || lw.seg == 4 || lw.seg == 8) return rounds(lw.seg) > 0 ? lw.seg : 1;
   if (lw.qpw != 0 || (lw.mode != 0 && lw.mode != 1)) return 1;
   int best = 1;
   double cbest = 255.0 * N;
   for (int S = 2; S <= 8; S <<= 1) {
-    if (!fits(S)) continue;
-    const double c = 350.0 * ((N + S - 1) / S) + 230.0 * (S - 1);
+    const int r = rounds(S);
+    if (r == 0) continue;
+    // per-pass chain x dispatch rounds (the sequential kernel keeps its grid resident: HBM scratch)
+    const double c = r * (350.0 * ((N + S - 1) / S) + 230.0 * (S - 1));
     if (c < cbest) {
       best = S;
       cbest = c;

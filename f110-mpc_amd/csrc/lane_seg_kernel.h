@@ -745,12 +745,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
 
 // Scratch of the segmented kernel for a batch: 1 fp64 (the lam-gains kept when they fit), 2 fp32
 // (references and scratch as float) when fp64 does not fit the CU's 160 KiB at the grid's waves
-// per CU, or when forced (lw.seg32: F110QP_LANE_SEG_F32=1); 0 if neither fits.
+// per CU (the float grid may then take more than one dispatch round), or when forced (lw.seg32:
+// F110QP_LANE_SEG_F32=1); 0 if neither fits.
 inline int seg_scratch_mode(const KParams& P, int B, int S, const LaneWork& lw) {
   const size_t waves = ((size_t)B * S + 63) / 64;
   const size_t per_cu = (waves + 255) / 256;
   const bool f64 = per_cu * seg_lds_bytes(P.N, S, false) <= 160 * 1024;
-  const bool f32 = per_cu * seg_lds_bytes(P.N, S, false, true) <= 160 * 1024;
+  const bool f32 = seg_lds_bytes(P.N, S, false, true) <= 160 * 1024;  // in one or more rounds
   if (lw.seg32 && f32) return 2;
   return f64 ? 1 : (f32 ? 2 : 0);
 }

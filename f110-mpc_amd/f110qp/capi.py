@@ -33,15 +33,17 @@ LANE_MIN_BATCH = 1024
 LANE_MIN_BATCH_WIDE = 1
 LANE_MIN_BATCH_GROUPED = LANE_MIN_BATCH
 LANE_MIN_BATCH_GROUPED_WIDE = LANE_MIN_BATCH_WIDE
+LANE_MAX_SMALL_BATCH = 8
 
 
 def auto_backend(horizon: int, batch: int, gap: bool, grouped: bool = False) -> int:
-    """The back end BACKEND_AUTO resolves to (mirrors lane_work() in f110qp_api.cpp)."""
+    """The back end BACKEND_AUTO resolves to (mirrors resolve_backend() in f110qp_api.cpp)."""
     if grouped:
         min_b = LANE_MIN_BATCH_GROUPED if horizon <= 32 else LANE_MIN_BATCH_GROUPED_WIDE
     else:
         min_b = LANE_MIN_BATCH if horizon <= 32 else LANE_MIN_BATCH_WIDE
-    return BACKEND_LANE if (not gap and batch >= min_b) else BACKEND_WAVE
+    small = not grouped and horizon <= 32 and batch <= LANE_MAX_SMALL_BATCH
+    return BACKEND_LANE if (not gap and (batch >= min_b or small)) else BACKEND_WAVE
 MAX_HORIZON = 48
 
 # every symbol include/f110qp.h declares

@@ -83,7 +83,8 @@ extern "C" {
 
 /* solver back ends (f110qp_config.backend) */
 #define F110QP_BACKEND_AUTO 0     /* lane-per-QP for box-only batches >= F110QP_LANE_MIN_BATCH  */
-                                  /* (N <= 32) or >= F110QP_LANE_MIN_BATCH_WIDE (N > 32)       */
+                                  /* or <= F110QP_LANE_MAX_SMALL_BATCH (N <= 32), and >=       */
+                                  /* F110QP_LANE_MIN_BATCH_WIDE (N > 32)                       */
 #define F110QP_BACKEND_WAVE 1     /* one wavefront per QP: condensed W = H^-1 + PDAS/GI         */
 #define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64; with gap rows the   */
                                   /* Riccati interior point (lane_ipm_kernel.h) where its LDS  */
@@ -103,6 +104,11 @@ extern "C" {
  * 1,041 us vs lane 240 us, round 2). */
 #define F110QP_LANE_MIN_BATCH 1024
 #define F110QP_LANE_MIN_BATCH_WIDE 1
+/* ... and, at N <= 32, batches of at most this many QPs (the single QP of MPC::Update): the
+ * partitioned-horizon lane kernel splits each horizon over S = 4 lanes and beats the wave kernel's
+ * one-QP chain (round 4, kernel us, N = 20: B = 1 lane 10.3 vs wave 19.3, B = 4 20.5 vs 23.9,
+ * B = 16 25.8 vs 25.5, B = 64 30.8 vs 25.2; tools/latency_probe.py) */
+#define F110QP_LANE_MAX_SMALL_BATCH 8
 #define F110QP_LANE_MIN_BATCH_GROUPED F110QP_LANE_MIN_BATCH
 #define F110QP_LANE_MIN_BATCH_GROUPED_WIDE F110QP_LANE_MIN_BATCH_WIDE
 

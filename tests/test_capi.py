@@ -143,8 +143,18 @@ def test_capi_raises_when_library_missing(monkeypatch):
 
 
 def test_auto_backend_policy(capi):
-    """BACKEND_AUTO: the wave kernel for small box batches and for gap rows, the lane kernel
-    from the measured crossover (1,024 QPs at N <= 32; every batch at N > 32)."""
+    """BACKEND_AUTO: the wave kernel for mid-size box batches and for gap rows, the lane kernel
+    from the measured crossover (1,024 QPs at N <= 32; every batch at N > 32) and for the single
+    QP of MPC::Update (up to 8 QPs at N <= 32: the partitioned horizon beats one QP's wave chain),
+    mirrored by the library's own resolution (f110qp_backend_info)."""
+    for B in (1, 4, 8):
+        assert capi.auto_backend(20, B, False) == capi.BACKEND_LANE
+    assert capi.auto_backend(20, 9, False) == capi.BACKEND_WAVE
+    s = capi.Solver(capi.default_config(20))
+    for B in (1, 8, 9, 512, 1023, 1024, 4096):
+        assert s.backend_info(B)[0] == capi.auto_backend(20, B, False), B
+    assert s.lane_segments(1) == 4
+    s.close()
     assert capi.auto_backend(20, 512, False) == capi.BACKEND_WAVE
     assert capi.auto_backend(20, 1023, False) == capi.BACKEND_WAVE
     assert capi.auto_backend(20, 1024, False) == capi.BACKEND_LANE
@@ -161,6 +171,7 @@ def test_auto_backend_grouped_policy(capi):
     assert capi.auto_backend(40, 65536, False, grouped=True) == capi.BACKEND_LANE
     assert capi.auto_backend(40, 1, False, grouped=True) == capi.BACKEND_LANE
     assert capi.auto_backend(20, 1023, False, grouped=True) == capi.BACKEND_WAVE
+    assert capi.auto_backend(20, 1, False, grouped=True) == capi.BACKEND_WAVE  # grouped: thresholds only
 
 
 def test_qp_dims_match_reference_sizes(capi, oracle):
@@ -195,9 +206,11 @@ def test_backend_info_resolves_auto_and_scratch(capi):
     # fp64 scratch at 16,384 x N = 30 would need 222 KB of LDS per CU: float scratch, S = 4
     assert s30.lane_segments(16384) == 4 and s30.backend_info(16384)[2] == 2
     # the middle of the C4 curve (65,536 over 4 / 2 GPUs): 16,384 x N = 40 on fp32 LDS scratch at
-    # S = 4; 32,768 does not fit four waves per CU and keeps the HBM-scratch sequential kernel
+    # S = 4 in one dispatch round, 32,768 at S = 4 in two (four of its eight waves per CU fit the
+    # LDS at once), 65,536 keeps the HBM-scratch sequential kernel
     assert s40.lane_segments(16384) == 4 and s40.backend_info(16384) == (capi.BACKEND_LANE, 16, 2)
-    assert s40.lane_segments(32768) == 1 and s40.backend_info(32768)[2] == 4
+    assert s40.lane_segments(32768) == 4 and s40.backend_info(32768)[2] == 2
+    assert s40.lane_segments(65536) == 1 and s40.backend_info(65536)[2] == 4
     s30.close()
     s25.close()
     assert s40.backend_info(65536, grouped=True) == (capi.BACKEND_LANE, 64, 4)
