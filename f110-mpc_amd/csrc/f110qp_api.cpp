@@ -106,6 +106,7 @@ struct f110qp_ctx {
   int lane_dref = 1;         // lane fp64 references in LDS when they fit (LaneWork::dref)
   int lane_seg = 0;          // lane horizon segments per QP (LaneWork::seg: 0 auto, 1 off, 2/4/8)
   int lane_seg32 = 0;        // segmented kernel: force fp32 references + scratch (LaneWork::seg32)
+  int gap_screen = -1;      // gap rows, AUTO: box screen on the lane kernel (-1 by batch, 0 off, 1 on)
   hipStream_t stream = nullptr;
 };
 
@@ -221,6 +222,7 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
   }
   // test hook: F110QP_LANE_SEG_F32=1 forces the segmented kernel's float references and scratch
   if (const char* ef = std::getenv("F110QP_LANE_SEG_F32")) c->lane_seg32 = std::atoi(ef) != 0;
+  if (const char* eg = std::getenv("F110QP_GAP_SCREEN")) c->gap_screen = std::atoi(eg) != 0;
   // test hook: F110QP_PDAS_MAX caps the wave kernel's box PDAS passes (0 = GI from scratch)
   k.pdas_max = 10;
   if (const char* ep = std::getenv("F110QP_PDAS_MAX")) {
@@ -303,7 +305,16 @@ static int resolve_backend(f110qp_ctx* c, int batch, bool grouped, const f110qp:
   return be;
 }
 
-// Back end of a call and, for the lane back end, its workspace.
+// Gap rows on the wave back end: does the call take the box screen on the lane kernel first
+// (F110QP_GAP_SCREEN_MIN_BATCH; AUTO only, ungrouped, no warm-start state)?
+static bool gap_screen(const f110qp_ctx* c, int batch, bool grouped) {
+  if (c->cfg.gap_mode != F110QP_GAP_ACTIVE || c->cfg.backend != F110QP_BACKEND_AUTO || grouped ||
+      c->cfg.warm_start || c->gap_screen == 0)
+    return false;
+  return c->gap_screen == 1 || batch >= F110QP_GAP_SCREEN_MIN_BATCH;
+}
+
+// Back end of a call and, for the lane back end (or the gap screen), its workspace.
 static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110qp::LaneWork* lw,
                      bool grouped = false) {
   *lw = f110qp::LaneWork();
@@ -325,9 +336,11 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
     if ((e = c->hand.ensure(((size_t)batch + 1) * sizeof(int))) != hipSuccess)
       return hip_fail(e, "hipMalloc hand-over list");
     lw->hand = (int*)c->hand.p;
+    lw->screen = *backend == f110qp::BACKEND_WAVE && gap_screen(c, batch, grouped);
+    if (!lw->screen) return F110QP_OK;
+  } else if (*backend == f110qp::BACKEND_WAVE) {
     return F110QP_OK;
   }
-  if (*backend == f110qp::BACKEND_WAVE) return F110QP_OK;
   // HBM scratch of ceil(B/L) waves x N stages x 8 values x L lanes (<= (B + 63) x N x 8 doubles)
   const size_t N = (size_t)c->cfg.horizon;
   e = c->lscr.ensure(((size_t)batch + 63) * N * 8 * sizeof(double));
@@ -490,6 +503,15 @@ int f110qp_lane_segments(f110qp_ctx* c, int batch, int* segments) {
   if (be != F110QP_BACKEND_LANE) *segments = 1;
   else if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) *segments = f110qp::lane_ipm_segments(c->kp, batch, lw);
   else *segments = f110qp::lane_segments(c->kp, batch, lw);
+  return F110QP_OK;
+}
+
+int f110qp_gap_screen(f110qp_ctx* c, int batch, int* on) {
+  if (!c || !on) return fail(F110QP_ERR_INVALID, "ctx / on is NULL");
+  if (batch < 1) return fail(F110QP_ERR_INVALID, "batch must be >= 1");
+  f110qp::LaneWork lw;
+  lw.seg = c->lane_seg;
+  *on = resolve_backend(c, batch, false, lw) == F110QP_BACKEND_WAVE && gap_screen(c, batch, false);
   return F110QP_OK;
 }
 

@@ -68,6 +68,8 @@ struct LaneWork {
   int seg = 0;    // horizon segments per QP (lane_seg_kernel.h): 0 auto, 1 off, 2 / 4 / 8 forced
   int seg32 = 0;  // segmented kernel: 1 forces float references and Riccati scratch in LDS
   int* hand = nullptr;  // gap rows: hand-over count (hand[0]) + list (hand + 1, B ints)
+  int screen = 0;       // gap rows, wave back end: box solve on the lane kernel first, GI only
+                        // for the QPs whose box optimum violates a gap row (f110qp_kernels.hip)
   IpmKnobs ipm;
 };
 

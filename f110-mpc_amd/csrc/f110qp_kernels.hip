@@ -38,6 +38,39 @@ static hipError_t launch_g(const KParams& P, int B, const float* x0, const float
 // waves of the hand-over launch (a work loop over the list; one per CU)
 constexpr int kHandGrid = 256;
 
+// Gap-row screen after a box-only lane solve: a QP whose box optimum keeps every gap row of stages
+// 1..N strictly satisfied has that point as its optimum with the gap rows (adding constraints that
+// hold at the unique minimiser of a strictly convex QP does not move it), so its lane outputs stand.
+// Every other QP goes on the list for the wave kernel's GI: a gap row violated or within the
+// margin, the stage-0 rows violated (constant rows, x0 on both lines by constraints.cpp:233-246;
+// violated, the wedge is infeasible), a non-SOLVED
+// box status, non-finite values. The margin is 1e-6 of the row's terms: ~8x the float rounding of
+// the stored x (absolute coordinates) plus the row's float data.
+__global__ __launch_bounds__(256) void gap_screen_kernel(const int B, const int N,
+                                                         const float* __restrict__ x0g,
+                                                         const float* __restrict__ hsg,
+                                                         const float* __restrict__ xo,
+                                                         const int* __restrict__ status,
+                                                         int* __restrict__ count, int* __restrict__ list) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  bool ok = status[b] == F110QP_SOLVED_ID;
+  const double px = (double)x0g[3 * b], py = (double)x0g[3 * b + 1];
+  const float* xb = xo + (size_t)b * (N + 1) * 3;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const double a = (double)hsg[6 * b + 3 * h], bb = (double)hsg[6 * b + 3 * h + 1],
+                 c = (double)hsg[6 * b + 3 * h + 2];
+    ok = ok && (a * px + bb * py >= -c - 1e-9);  // stage 0: constant rows
+    for (int i = 1; i <= N && ok; i++) {
+      const double x = (double)xb[3 * i], y = (double)xb[3 * i + 1];
+      const double ax = a * x, by = bb * y;
+      ok = (ax + by + c >= 1e-6 * (1.0 + fabs(ax) + fabs(by) + fabs(c)));
+    }
+  }
+  if (!ok) list[atomicAdd(count, 1)] = b;
+}
+
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
                         const float* xr, const float* hs, float* uo, float* xo, int* st,
                         int* its, const WarmState& ws, int backend, const LaneWork& lw,
@@ -51,6 +84,20 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
     if ((e = launch_lane_ipm(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s)) != hipSuccess) return e;
     return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 1,
                           lw.hand, B < kHandGrid ? B : kHandGrid, oo, s);
+  }
+  if (hs && lw.screen) {
+    // box-only lane solve of every QP, the screen, GI over the QPs it lists (grid B: the waves
+    // past the device-side count exit at once), then the fp64 re-check as below
+    hipError_t e = launch_lane(P, B, x0, ul, xr, uo, xo, st, its, WarmState(), lw, oo, s);
+    if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(lw.hand, 0, sizeof(int), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st,
+                       lw.hand, lw.hand + 1);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 1,
+                       lw.hand, B, oo, s);
+    if (e != hipSuccess) return e;
+    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s);
   }
   if (hs) {
     hipError_t e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,

@@ -332,6 +332,8 @@ struct Smem {
 // 2 gap row (stage var/2+1, side var&1)
 __device__ __forceinline__ float box_sign(int id) { return (id - 3 * (id / 3) == 0) ? 1.f : -1.f; }
 
+constexpr int kTriBlock = 8;  // steps per block of the triangular solves (loads hoisted)
+
 // l = L^-1 v, one lane per active slot (slot j: lane j mod 64, row j / 64); L read from LDS.
 // A plain q-step loop: the slot count is uniform, each step is mul -> readlane -> fma.
 template <int NUM, bool GAP, int R>
@@ -348,7 +350,26 @@ __device__ __forceinline__ void tri_forward(Smem<NUM, GAP>& sm, int lane, int q,
     Lrow[r] = sm.L[row < NUM ? row : NUM - 1];
   }
   const int q0 = q < 64 ? q : 64;
-  for (int kk = 0; kk < q0; kk++) {
+  // blocks of kTriBlock steps with the block's L loads issued first, off the dependent
+  // mul -> readlane -> fma chain (readlane is convergent: the compiler does not runtime-unroll
+  // the rolled loop, whose every step then waits for its own LDS load)
+  int kk = 0;
+  for (; kk + kTriBlock <= q0; kk += kTriBlock) {
+    float lb[kTriBlock][R];
+#pragma unroll
+    for (int j = 0; j < kTriBlock; j++)
+#pragma unroll
+      for (int r = 0; r < R; r++) lb[j][r] = Lrow[r][kk + j];
+#pragma unroll
+    for (int j = 0; j < kTriBlock; j++) {
+      const float t = acc[0] * rdiag[0];
+      const float lk = readlane_f(t, kk + j);
+      lv[0] = (lane == kk + j) ? t : lv[0];
+#pragma unroll
+      for (int r = 0; r < R; r++) acc[r] = fmaf(-lb[j][r], lk, acc[r]);
+    }
+  }
+  for (; kk < q0; kk++) {
     const float t = acc[0] * rdiag[0];
     const float lk = readlane_f(t, kk);
     lv[0] = (lane == kk) ? t : lv[0];
@@ -390,7 +411,20 @@ __device__ __forceinline__ void tri_backward(Smem<NUM, GAP>& sm, int lane, int q
     }
   }
   const int q0 = q < 64 ? q : 64;
-  for (int jj = q0 - 1; jj >= 0; jj--) {
+  int jj = q0 - 1;
+  for (; jj - kTriBlock + 1 >= 0; jj -= kTriBlock) {  // blocks as in tri_forward
+    float lb[kTriBlock];
+#pragma unroll
+    for (int j = 0; j < kTriBlock; j++) lb[j] = sm.L[jj - j][col[0]];
+#pragma unroll
+    for (int j = 0; j < kTriBlock; j++) {
+      const float t = acc[0] * rdiag[0];
+      const float rj = readlane_f(t, jj - j);
+      out[0] = (lane == jj - j) ? t : out[0];
+      acc[0] = fmaf(-lb[j], rj, acc[0]);
+    }
+  }
+  for (; jj >= 0; jj--) {
     const float t = acc[0] * rdiag[0];
     const float rj = readlane_f(t, jj);
     out[0] = (lane == jj) ? t : out[0];
@@ -1522,7 +1556,23 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           float dx[R];
 #pragma unroll
           for (int r = 0; r < R; r++) dx[r] = -w1[r];
-          for (int j = 0; j < q; j++) {
+          int j = 0;
+          if constexpr (GAP) {  // V rows in blocks, loads first (as the GI step's z update)
+            for (; j + kTriBlock <= q; j += kTriBlock) {
+              float vb[kTriBlock][R];
+#pragma unroll
+              for (int jb = 0; jb < kTriBlock; jb++)
+#pragma unroll
+                for (int r = 0; r < R; r++) vb[jb][r] = sm.V[j + jb][cl[r]];
+#pragma unroll
+              for (int jb = 0; jb < kTriBlock; jb++) {
+                const float duj = rl_f<R>(du, j + jb);
+#pragma unroll
+                for (int r = 0; r < R; r++) dx[r] = fmaf(duj, vb[jb][r], dx[r]);
+              }
+            }
+          }
+          for (; j < q; j++) {
             const float duj = rl_f<R>(du, j);
             const int sj = GAP ? 0 : rl_i<R>(slot_id, j);
 #pragma unroll
@@ -1661,7 +1711,23 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       float z[R];
 #pragma unroll
       for (int r = 0; r < R; r++) z[r] = w[r];
-      for (int j = 0; j < q; j++) {
+      int j = 0;
+      if constexpr (GAP) {  // V rows in blocks: the block's loads first (see tri_forward)
+        for (; j + kTriBlock <= q; j += kTriBlock) {
+          float vb[kTriBlock][R];
+#pragma unroll
+          for (int jb = 0; jb < kTriBlock; jb++)
+#pragma unroll
+            for (int r = 0; r < R; r++) vb[jb][r] = sm.V[j + jb][cl[r]];
+#pragma unroll
+          for (int jb = 0; jb < kTriBlock; jb++) {
+            const float rj = rl_f<R>(rr, j + jb);
+#pragma unroll
+            for (int r = 0; r < R; r++) z[r] = fmaf(-rj, vb[jb][r], z[r]);
+          }
+        }
+      }
+      for (; j < q; j++) {
         const float rj = rl_f<R>(rr, j);
         const int sj = GAP ? 0 : rl_i<R>(slot_id, j);
 #pragma unroll

@@ -34,6 +34,7 @@ LANE_MIN_BATCH_WIDE = 1
 LANE_MIN_BATCH_GROUPED = LANE_MIN_BATCH
 LANE_MIN_BATCH_GROUPED_WIDE = LANE_MIN_BATCH_WIDE
 LANE_MAX_SMALL_BATCH = 8
+GAP_SCREEN_MIN_BATCH = 1024
 
 
 def auto_backend(horizon: int, batch: int, gap: bool, grouped: bool = False) -> int:
@@ -44,6 +45,13 @@ def auto_backend(horizon: int, batch: int, gap: bool, grouped: bool = False) -> 
         min_b = LANE_MIN_BATCH if horizon <= 32 else LANE_MIN_BATCH_WIDE
     small = not grouped and horizon <= 32 and batch <= LANE_MAX_SMALL_BATCH
     return BACKEND_LANE if (not gap and (batch >= min_b or small)) else BACKEND_WAVE
+
+
+def auto_gap_screen(batch: int, grouped: bool = False, warm_start: bool = False) -> bool:
+    """Whether AUTO takes the box screen for a gap-row call (mirrors gap_screen() in f110qp_api.cpp)."""
+    return not grouped and not warm_start and batch >= GAP_SCREEN_MIN_BATCH
+
+
 MAX_HORIZON = 48
 
 # every symbol include/f110qp.h declares
@@ -75,6 +83,7 @@ EXPORTED = (
     "f110qp_select_dev",
     "f110qp_backend_info",
     "f110qp_lane_segments",
+    "f110qp_gap_screen",
 )
 SCRATCH_NAMES = {0: "none (wave back end)", 1: "LDS fp64", 2: "LDS fp32", 3: "HBM fp64", 4: "HBM fp32"}
 
@@ -143,6 +152,7 @@ def load():
     L.f110qp_select_dev.argtypes = [C.c_int, fp, C.c_int, fp, fp, fp, fp, fp]
     L.f110qp_backend_info.argtypes = [C.c_void_p, C.c_int, C.c_int] + [C.POINTER(C.c_int)] * 3
     L.f110qp_lane_segments.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    L.f110qp_gap_screen.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
     L.f110qp_warm_reset.argtypes = [C.c_void_p]
     L.f110qp_qp_dims.argtypes = [C.c_int] + [C.POINTER(C.c_int)] * 4
@@ -270,6 +280,13 @@ class Solver:
         v = C.c_int()
         _check(self.lib.f110qp_lane_segments(self._h, int(batch), C.byref(v)), "f110qp_lane_segments")
         return v.value
+
+    def gap_screen(self, batch: int) -> bool:
+        """Does a gap-row solve call of `batch` QPs take the box screen on the lane back end before
+        the wave kernel's GI (f110qp_gap_screen)?"""
+        v = C.c_int()
+        _check(self.lib.f110qp_gap_screen(self._h, int(batch), C.byref(v)), "f110qp_gap_screen")
+        return bool(v.value)
 
     def solve(self, x0, u_lin, x_ref, halfspace=None, objective=False):
         """Host arrays in, host arrays out (synchronous). Returns (u[B,N,2], x[B,N+1,3],

@@ -109,6 +109,12 @@ extern "C" {
  * one-QP chain (round 4, kernel us, N = 20: B = 1 lane 10.3 vs wave 19.3, B = 4 20.5 vs 23.9,
  * B = 16 25.8 vs 25.5, B = 64 30.8 vs 25.2; tools/latency_probe.py) */
 #define F110QP_LANE_MAX_SMALL_BATCH 8
+/* Gap rows (gap_mode ACTIVE), AUTO, ungrouped, no warm start, batches of at least this many QPs:
+ * the box-only problem is solved on the lane back end first, and only the QPs whose box optimum
+ * leaves a gap row violated (or within a 1e-6 margin) go to the wave kernel's GI; the others'
+ * lane outputs are the optimum with the gap rows as well (round 4: 57% of the C3 batch). Results
+ * are the exact optimum either way; the iteration count is the lane PDAS passes for screened QPs. */
+#define F110QP_GAP_SCREEN_MIN_BATCH 1024
 #define F110QP_LANE_MIN_BATCH_GROUPED F110QP_LANE_MIN_BATCH
 #define F110QP_LANE_MIN_BATCH_GROUPED_WIDE F110QP_LANE_MIN_BATCH_WIDE
 
@@ -227,6 +233,12 @@ int f110qp_backend_info(f110qp_ctx* ctx, int batch, int grouped, int* backend, i
  * distinct QPs; with gap rows on the lane back end the interior point's S = 2..16).
  * The result is the exact optimum either way. */
 int f110qp_lane_segments(f110qp_ctx* ctx, int batch, int* segments);
+
+/* on = 1 when a gap-row call of `batch` QPs takes the box screen (F110QP_GAP_SCREEN_MIN_BATCH):
+ * the lane back end solves the box-only problem, the wave kernel's GI only the QPs whose box
+ * optimum does not keep every gap row (an ungrouped solve call; replaces nothing in the reference:
+ * a query of this library's dispatch, like f110qp_backend_info). */
+int f110qp_gap_screen(f110qp_ctx* ctx, int batch, int* on);
 
 /* Forget the warm-start state of every slot (the next call solves cold). */
 int f110qp_warm_reset(f110qp_ctx* ctx);
