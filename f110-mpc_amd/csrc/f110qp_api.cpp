@@ -216,6 +216,10 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     if (v >= 0 && v <= 200) c->ipm.max_iter = v;
   }
   if (const char* ev = std::getenv("F110QP_IPM_DEBUG")) c->ipm.debug = std::atoi(ev);
+  if (const char* ev = std::getenv("F110QP_IPM_ACTSIG")) {
+    const double v = std::atof(ev);
+    if (v > 0.0) c->ipm.act_sig = v;
+  }
   if (const char* ev = std::getenv("F110QP_IPM_SFLOOR")) {
     const double v = std::atof(ev);
     if (v > 0.0) c->ipm.s_floor = v;

@@ -51,6 +51,7 @@ struct IpmKnobs {
   double tolp = 1e-9;    // polish acceptance: row violation, x (1 + |bound|)
   double told = 1e-9;    // polish acceptance: multiplier sign of an active row
   double tau = 0.995;    // fraction to the boundary
+  double act_sig = 1e4;  // polish: a row is guessed active when z > act_sig * s (Sig = z / s >= act_sig)
   double s_floor = 1.0;  // initial slack floor
   int max_iter = 30;     // interior-point iterations before the hand-over to the wave kernel
   int debug = 0;         // test hook: return every QP's current iterate as SOLVED (no polish test)

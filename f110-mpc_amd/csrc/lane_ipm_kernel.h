@@ -21,7 +21,7 @@
 // per factor, then a vector-only pass per further right-hand side).
 //
 // Polish (OSQP's `polish`, here the exit test): once a QP's mu is small it guesses the active rows
-// A = {z > s} and solves the equality QP on them by an augmented Lagrangian on the SAME factor
+// A = {z > 1e4 s} and solves the equality QP on them by an augmented Lagrangian on the SAME factor
 // (penalty Sig_j, multipliers started at z_j; inactive rows act as proximal terms that vanish at
 // convergence): two linear-only solves. The QP is SOLVED when every inactive row holds
 // (c >= -tol), every active row holds with equality (|c| <= tol) and carries a multiplier >= -tol:
@@ -29,6 +29,13 @@
 // interior point has not polished after IpmKnobs::max_iter iterations (primal infeasible, or a stalled
 // path) goes on the hand-over list: the wave kernel's Goldfarb-Idnani loop solves it or proves
 // infeasibility (status -3), exactly as before. Design model: tests/diag_ipm_model.py.
+// The factor 1e4 (IpmKnobs::act_sig, was 1): a degenerate row whose z and s both go to zero
+// (z ~ s ~ sqrt(mu)) carries Sig ~ 1, too small a penalty for the two AL steps to pin it, and
+// with z > s it failed the multiplier sign test at every iterate (an N = 48 gap QP that neither
+// this polish nor GI certified; numpy model first: acceptance up on 4 test batches at 1e2..1e6
+// with no accuracy change; on the device, at S = 16, 1e4 accepted it and 1e2 did not); such a
+// row is taken as inactive, and an active row's penalty is then large enough for the two AL
+// steps' convergence test to mean stationarity.
 //
 // Layout: LDS per wave, lane-major rows (every access one conflict-free 64-lane row), fp64:
 // references [3m][64], per-stage fields [m][kIpmNF][64], the segment-end state [39][64].
@@ -553,9 +560,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_IPM_W
         } else if constexpr (MODE == 1) {
           e[j] = sg[j] * (cc[j] - sj) + (F(t, kFDsDz + j) - smu) * is;
         } else if constexpr (MODE == 2) {
-          e[j] = zj > sj ? sg[j] * cc[j] - zj : 0.0;
+          e[j] = zj > kn.act_sig * sj ? sg[j] * cc[j] - zj : 0.0;
         } else {
-          e[j] = zj > sj ? 2.0 * sg[j] * cc[j] - zj : 0.0;
+          e[j] = zj > kn.act_sig * sj ? 2.0 * sg[j] * cc[j] - zj : 0.0;
         }
       }
       // x_{i+1}'s gap rows: Hessian (FAC) and linear term
@@ -738,7 +745,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_IPM_W
 #pragma unroll
         for (int j = 0; j < 6; j++) {
           const double sj = F(t, kFS + j), zj = F(t, kFZ + j);
-          const bool act = zj > sj;
+          const bool act = zj > kn.act_sig * sj;
           const double sgj = zj * ipm_rcp1(sj);
           const double y2 = zj - sgj * (c1v[j] + c2v[j]);
           const bool oka = (y2 >= -kn.told) & (fabs(c2v[j]) <= kn.tolp * scl[j]);

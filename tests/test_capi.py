@@ -174,6 +174,22 @@ def test_auto_backend_grouped_policy(capi):
     assert capi.auto_backend(20, 1, False, grouped=True) == capi.BACKEND_WAVE  # grouped: thresholds only
 
 
+def test_gap_screen_policy(capi):
+    """Gap rows under AUTO take the box screen on the lane back end from F110QP_GAP_SCREEN_MIN_BATCH
+    QPs (ungrouped, no warm start); an explicit back end never does. Mirrored by capi.auto_gap_screen."""
+    sg = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE))
+    for B in (1, 512, 1023, 1024, 4096, 65536):
+        assert sg.gap_screen(B) == capi.auto_gap_screen(B) == (B >= capi.GAP_SCREEN_MIN_BATCH), B
+    sg.close()
+    for over in (dict(backend=capi.BACKEND_WAVE), dict(backend=capi.BACKEND_LANE), dict(warm_start=1)):
+        s = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE, **over))
+        assert not s.gap_screen(4096), over
+        s.close()
+    s = capi.Solver(capi.default_config(20))  # box rows: nothing to screen
+    assert not s.gap_screen(4096)
+    s.close()
+
+
 def test_qp_dims_match_reference_sizes(capi, oracle):
     """f110qp_qp_dims: the reference's n = 5N+3, m = 7N+5 (src/mpc.cpp:26-29) and the stored
     nonzeros of P and A, equal to the oracle's assembly for every horizon."""

@@ -1,0 +1,77 @@
+"""The gap-row box screen (f110qp_kernels.hip gap_screen_kernel): AUTO gap calls of >= 1,024 QPs
+solve the box-only problem on the lane back end and send to the wave kernel's GI only the QPs
+whose box optimum leaves a gap row violated or within the margin. Same contract as
+test_gpu_parity.py against the oracle: identical status per QP, and ||u - u*||_inf /
+max(1, ||u*||_inf) <= 1e-4 (same for x) for SOLVED.
+"""
+import numpy as np
+import pytest
+from test_gpu_parity import check, halfspaces_oracle, rel_err
+
+from f110qp import workload
+
+pytestmark = pytest.mark.gpu
+
+
+def _gap_batch(oracle, B, N, seed, **kw):
+    w = workload.make_batch(B, N, seed=seed, **kw)
+    ranges, *geom = workload.make_scans(B, seed=seed)
+    return w, halfspaces_oracle(oracle, w["x0"], ranges, geom)
+
+
+def test_screen_c3_full_batch(oracle, capi):
+    """BASELINE configs[2] (4,096 x N = 20 with gap rows) on the AUTO path, which screens."""
+    s = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE))
+    assert s.gap_screen(4096)
+    s.close()
+    w, hs = _gap_batch(oracle, 4096, 20, 2025)
+    u, x, st, it = check(oracle, capi, 20, w, hs, gap=True)
+    assert (st == capi.SOLVED).mean() > 0.99
+
+
+@pytest.mark.parametrize("N", [5, 13, 30, 40, 48])
+def test_screen_horizons(oracle, capi, N):
+    w, hs = _gap_batch(oracle, 1024, N, 600 + N)
+    check(oracle, capi, N, w, hs, gap=True)
+
+
+def test_screen_agrees_with_wave_only(oracle, capi):
+    """Screened and unscreened (explicit wave back end) runs of one batch: same statuses, the same
+    optimum to the tolerance."""
+    N, B = 20, 2048
+    w, hs = _gap_batch(oracle, B, N, 91, lateral=0.8)
+    out = {}
+    for name, be in (("auto", capi.BACKEND_AUTO), ("wave", capi.BACKEND_WAVE)):
+        s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE, backend=be))
+        out[name] = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
+        s.close()
+    np.testing.assert_array_equal(out["auto"][2], out["wave"][2])
+    ok = out["wave"][2] == capi.SOLVED
+    assert rel_err(out["auto"][0][ok], out["wave"][0][ok].astype(np.float64)).max() <= 1e-4
+
+
+def test_screen_infeasible_and_non_finite(oracle, capi, monkeypatch):
+    """Forced on a small batch (F110QP_GAP_SCREEN=1): infeasible wedges (stage-0 rows violated or
+    an empty feasible set) and non-finite inputs pass through to GI and keep their statuses."""
+    from test_oracle import infeasible_cases
+
+    monkeypatch.setenv("F110QP_GAP_SCREEN", "1")
+    N, B = 20, 96
+    w, hs = _gap_batch(oracle, B, N, 12)
+    for i, (x0, h) in enumerate(infeasible_cases()):
+        w["x0"][3 + 10 * i] = x0
+        w["u_lin"][3 + 10 * i] = [4.5, 0.0]
+        hs[3 + 10 * i] = h
+    a0, b0, c0 = (float(v) for v in hs[40, 0])  # x0 0.5 outside the first half-space: stage-0 row violated
+    hs[40, 0, 2] = c0 - (a0 * float(w["x0"][40, 0]) + b0 * float(w["x0"][40, 1]) + c0) - 0.5
+    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE))
+    assert s.gap_screen(B)
+    s.close()
+    u, x, st, it = check(oracle, capi, N, w, hs, gap=True)
+    assert st[40] == capi.PRIMAL_INFEASIBLE
+    w["x0"][5, 0] = np.nan
+    hs[9, 1, 1] = np.inf
+    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE))
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
+    s.close()
+    assert st[5] == capi.NUMERICAL and st[9] == capi.NUMERICAL
