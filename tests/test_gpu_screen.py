@@ -71,7 +71,12 @@ def test_screen_infeasible_and_non_finite(oracle, capi, monkeypatch):
     assert st[40] == capi.PRIMAL_INFEASIBLE
     w["x0"][5, 0] = np.nan
     hs[9, 1, 1] = np.inf
-    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE))
-    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
-    s.close()
-    assert st[5] == capi.NUMERICAL and st[9] == capi.NUMERICAL
+    out = {}
+    for name, be in (("auto", capi.BACKEND_AUTO), ("wave", capi.BACKEND_WAVE)):
+        s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE, backend=be))
+        out[name] = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
+        s.close()
+    st = out["auto"][2]
+    # non-finite state: NUMERICAL; a non-finite gap row: the wave kernel's empty-set verdict
+    assert st[5] == capi.NUMERICAL and st[9] == capi.PRIMAL_INFEASIBLE
+    np.testing.assert_array_equal(st, out["wave"][2])
