@@ -97,7 +97,7 @@ struct f110qp_ctx {
   DevBuf gW, gkey, glead;    // grouped mode: W = H^-1, key and leader per group
   DevBuf dgrp;               // host-pointer grouped calls: device copy of the group ids
   DevBuf lscr;               // lane back end: HBM Riccati scratch (when not in LDS)
-  DevBuf hand;               // lane back end, gap rows: hand-over count + list (B + 1 ints)
+  DevBuf hand;               // gap rows: two counts + one list (B + 2 ints; LaneWork::hand)
   f110qp::IpmKnobs ipm;      // lane back end, gap rows: interior-point knobs (test/bench hooks)
   int lane_kmax = 16;        // lane back end: PDAS passes before single (least-index) flips
   int lane_mode = 0;         // lane scratch placement (LaneWork::mode)
@@ -337,7 +337,7 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) {
     // count + list of the interior point's hand-over (lane back end) or of the fp64 re-check of
     // the wave kernel's non-SOLVED QPs (wave back end)
-    if ((e = c->hand.ensure(((size_t)batch + 1) * sizeof(int))) != hipSuccess)
+    if ((e = c->hand.ensure(((size_t)batch + 2) * sizeof(int))) != hipSuccess)
       return hip_fail(e, "hipMalloc hand-over list");
     lw->hand = (int*)c->hand.p;
     lw->screen = *backend == f110qp::BACKEND_WAVE && gap_screen(c, batch, grouped);

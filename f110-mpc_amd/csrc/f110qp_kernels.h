@@ -68,7 +68,8 @@ struct LaneWork {
   int dref = 1;   // 1: fp64 references in LDS when the resident waves fit (DREF); 0: float
   int seg = 0;    // horizon segments per QP (lane_seg_kernel.h): 0 auto, 1 off, 2 / 4 / 8 forced
   int seg32 = 0;  // segmented kernel: 1 forces float references and Riccati scratch in LDS
-  int* hand = nullptr;  // gap rows: hand-over count (hand[0]) + list (hand + 1, B ints)
+  int* hand = nullptr;  // gap rows: two counts (hand[0]: hand-over / screen, hand[1]: the fp64
+                        // re-check) + one list (hand + 2, B ints) the two use one after the other
   int screen = 0;       // gap rows, wave back end: box solve on the lane kernel first, GI only
                         // for the QPs whose box optimum violates a gap row (f110qp_kernels.hip)
   IpmKnobs ipm;
@@ -81,6 +82,11 @@ struct LaneWork {
 struct ObjOut {
   double* obj = nullptr;
   double* cost = nullptr;
+  // gap-row box screen fused into the segmented lane kernel's output sweep (f110qp_kernels.hip):
+  // the half-spaces, and the count + list the QPs that need GI are appended to (null: no screen)
+  const float* scr_hs = nullptr;
+  int* scr_count = nullptr;
+  int* scr_list = nullptr;
 };
 
 // waves the lane kernel's grid aims for (one per CU of the MI355X's 256)
@@ -99,7 +105,7 @@ int lane_seg_scratch(const KParams& P, int B, int S, const LaneWork& lw);
 int lane_ipm_segments(const KParams& P, int B, const LaneWork& lw);
 
 // The interior-point lane kernel alone: QPs it does not polish are appended to the hand-over
-// list (lw.hand; the count must be zero on entry).
+// list (count lw.hand[0], list lw.hand + 2; the count must be zero on entry).
 hipError_t launch_lane_ipm(const KParams& P, int B, const float* x0, const float* u_lin,
                            const float* x_ref, const float* hs, float* u_out, float* x_out,
                            int* status, int* iters, const LaneWork& lw, const ObjOut& oo,
@@ -107,11 +113,12 @@ hipError_t launch_lane_ipm(const KParams& P, int B, const float* x0, const float
 
 // fp64 re-check of the wave kernel's gap-row QPs it did not report SOLVED (lane_ipm_inst.hip):
 // the interior point over their list; polished -> SOLVED, Farkas certificate -> PRIMAL_INFEASIBLE,
-// else the wave kernel's answer stands. Needs lw.hand (B + 1 ints).
+// else the wave kernel's answer stands. Needs lw.hand (B + 2 ints; count hand[1], zeroed by the
+// caller when `zeroed`).
 hipError_t launch_gap_recheck(const KParams& P, int B, const float* x0, const float* u_lin,
                               const float* x_ref, const float* hs, float* u_out, float* x_out,
                               int* status, int* iters, const LaneWork& lw, const ObjOut& oo,
-                              hipStream_t stream);
+                              hipStream_t stream, bool zeroed = false);
 
 enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
 

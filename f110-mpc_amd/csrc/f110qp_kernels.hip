@@ -82,22 +82,33 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
     hipError_t e = hipMemsetAsync(lw.hand, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     if ((e = launch_lane_ipm(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s)) != hipSuccess) return e;
-    return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 1,
+    return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 2,
                           lw.hand, B < kHandGrid ? B : kHandGrid, oo, s);
   }
   if (hs && lw.screen) {
-    // box-only lane solve of every QP, the screen, GI over the QPs it lists (grid B: the waves
-    // past the device-side count exit at once), then the fp64 re-check as below
-    hipError_t e = launch_lane(P, B, x0, ul, xr, uo, xo, st, its, WarmState(), lw, oo, s);
+    // one memset clears both counts (screen hand[0], re-check hand[1]); the box-only lane solve of
+    // every QP (the segmented kernel evaluates the screen in its output sweep, in fp64, and lists
+    // the QPs that need GI; the sequential kernel leaves it to gap_screen_kernel), GI over the
+    // list (grid B: the waves past the device-side count exit at once), the fp64 re-check
+    hipError_t e = hipMemsetAsync(lw.hand, 0, 2 * sizeof(int), s);
     if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(lw.hand, 0, sizeof(int), s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st,
-                       lw.hand, lw.hand + 1);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 1,
+    const bool fused = lane_segments(P, B, lw) > 1;
+    ObjOut so = oo;
+    if (fused) {
+      so.scr_hs = hs;
+      so.scr_count = lw.hand;
+      so.scr_list = lw.hand + 2;
+    }
+    if ((e = launch_lane(P, B, x0, ul, xr, uo, xo, st, its, WarmState(), lw, so, s)) != hipSuccess) return e;
+    if (!fused) {
+      hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st,
+                         lw.hand, lw.hand + 2);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 2,
                        lw.hand, B, oo, s);
     if (e != hipSuccess) return e;
-    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s);
+    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s, true);
   }
   if (hs) {
     hipError_t e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,

@@ -50,36 +50,37 @@ hipError_t launch_lane_ipm(const KParams& P, int B, const float* x0, const float
   if (B <= 0) return hipSuccess;
   const bool rot = lw.rot && P.q[0] == P.q[1];
   const int S = lane_ipm_segments(P, B, lw);
-  return rot ? ipm_s<true>(S, P, B, x0, ul, xr, hs, uo, xo, st, its, lw.hand + 1, lw.hand, lw.ipm, oo, s, nullptr,
+  return rot ? ipm_s<true>(S, P, B, x0, ul, xr, hs, uo, xo, st, its, lw.hand + 2, lw.hand, lw.ipm, oo, s, nullptr,
                            nullptr, 0)
-             : ipm_s<false>(S, P, B, x0, ul, xr, hs, uo, xo, st, its, lw.hand + 1, lw.hand, lw.ipm, oo, s, nullptr,
+             : ipm_s<false>(S, P, B, x0, ul, xr, hs, uo, xo, st, its, lw.hand + 2, lw.hand, lw.ipm, oo, s, nullptr,
                             nullptr, 0);
 }
 
 // Re-check of the wave kernel's gap-row QPs that are not SOLVED (status 2, -2, -3, -10): list them,
 // then run the interior point over the list in fp64; a polished point (KKT-checked) becomes SOLVED,
 // a Farkas certificate PRIMAL_INFEASIBLE, anything else keeps the wave kernel's answer. At most
-// kRecheckCap list items are re-checked (one wave per CU at S = 4, N = 20).
+// kRecheckCap list items are re-checked (one wave per CU at S = 4, N = 20). Count hand[1], list
+// hand + 2; zeroed: the caller's one memset already cleared hand[1].
 constexpr int kRecheckCap = 4096;
 hipError_t launch_gap_recheck(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                               const float* hs, float* uo, float* xo, int* st, int* its, const LaneWork& lw,
-                              const ObjOut& oo, hipStream_t s) {
+                              const ObjOut& oo, hipStream_t s, bool zeroed) {
   if (B <= 0 || !lw.hand) return hipSuccess;
   const int cap = B < kRecheckCap ? B : kRecheckCap;
   LaneWork l2 = lw;
   l2.seg = 0;
   const int S = lane_ipm_segments(P, cap, l2);
   if (S == 0) return hipSuccess;  // no segmentation fits this horizon: the wave kernel's answer stands
-  hipError_t e = hipMemsetAsync(lw.hand, 0, sizeof(int), s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(ipm_flag_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, st, lw.hand, lw.hand + 1);
+  hipError_t e = hipSuccess;
+  if (!zeroed && (e = hipMemsetAsync(lw.hand + 1, 0, sizeof(int), s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(ipm_flag_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, st, lw.hand + 1, lw.hand + 2);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const bool rot = lw.rot && P.q[0] == P.q[1];
   // grid of `cap` QPs; the kernel reads the count and idle waves exit at once
   return rot ? ipm_s<true>(S, P, cap, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, lw.ipm, oo, s,
-                           lw.hand + 1, lw.hand, 1)
+                           lw.hand + 2, lw.hand + 1, 1)
              : ipm_s<false>(S, P, cap, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, lw.ipm, oo, s,
-                            lw.hand + 1, lw.hand, 1);
+                            lw.hand + 2, lw.hand + 1, 1);
 }
 
 }  // namespace f110qp

@@ -11,7 +11,7 @@
 
 namespace f110qp {
 
-template <int S, bool ROT>
+template <int S, bool ROT, bool SCR>
 hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                              float* uo, float* xo, int* st, int* its, const WarmState& ws,
                              const LaneWork& lw, const ObjOut& oo, hipStream_t s);  // lane_seg_inst.hip
@@ -158,15 +158,20 @@ hipError_t launch_lane(const KParams& P, int B, const float* x0, const float* ul
                        const WarmState& ws, const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
   const bool rot = lw.rot && P.q[0] == P.q[1];
+  const bool scr = oo.scr_hs != nullptr;  // the gap-row screen variant (f110qp_kernels.hip)
+#define F110QP_SEG_CASE(S)                                                                        \
+  case S:                                                                                         \
+    return scr ? (rot ? launch_lane_seg_t<S, true, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s)  \
+                      : launch_lane_seg_t<S, false, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s)) \
+               : (rot ? launch_lane_seg_t<S, true, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s) \
+                      : launch_lane_seg_t<S, false, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s));
   switch (lane_segments(P, B, lw)) {
-    case 2: return rot ? launch_lane_seg_t<2, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s)
-                       : launch_lane_seg_t<2, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
-    case 4: return rot ? launch_lane_seg_t<4, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s)
-                       : launch_lane_seg_t<4, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
-    case 8: return rot ? launch_lane_seg_t<8, true>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s)
-                       : launch_lane_seg_t<8, false>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
+    F110QP_SEG_CASE(2)
+    F110QP_SEG_CASE(4)
+    F110QP_SEG_CASE(8)
     default: break;
   }
+#undef F110QP_SEG_CASE
   switch (lane_qps_per_wave(B, lw.qpw)) {
     case 1: return launch_lq<1>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
     case 2: return launch_lq<2>(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);

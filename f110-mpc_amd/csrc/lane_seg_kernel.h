@@ -94,7 +94,7 @@ __device__ __forceinline__ double seg_shfl(double v, int src) {
 // neutral (tools/ab_seg_variant.sh)
 #define F110QP_SEG_WPE 2
 #endif
-template <int S, bool ROT, bool FST, typename ST = double>
+template <int S, bool ROT, bool FST, typename ST = double, bool SCR = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_WPE, F110QP_SEG_WPE))) void lane_seg_kernel(
     const KParams P, const int B, const float* __restrict__ x0g, const float* __restrict__ ulg,
     const float* __restrict__ xrg, float* __restrict__ uout, float* __restrict__ xout,
@@ -651,6 +651,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     const double wt = rt + th0;
     Cr += 0.5 * (q0 * wx * wx + q1 * wy * wy + q2 * wt * wt);
   };
+  // gap-row box screen (f110qp_kernels.hip, AUTO gap calls): the box optimum is the optimum with
+  // the gap rows too when it keeps every row of stages 1..N with a margin of 1e-6 of the row's
+  // terms (evaluated here on the fp64 rollout in world coordinates) and the constant stage-0 rows
+  // hold; any other QP goes on the list for GI. A template variant (SCR): the box-only kernels
+  // keep their code (a runtime test cost C2 26.7 -> 27.5 us, same box)
+  double ga0 = 0.0, gb0 = 0.0, gc0 = 0.0, ga1 = 0.0, gb1 = 0.0, gc1 = 0.0;
+  if constexpr (SCR) {
+    const float* h6 = oo.scr_hs + 6 * (size_t)b;
+    ga0 = h6[0]; gb0 = h6[1]; gc0 = h6[2]; ga1 = h6[3]; gb1 = h6[4]; gc1 = h6[5];
+  }
+  bool gok = true;
   {
     double x0 = xs0, x1 = xs1, x2 = xs2;
     for (int t = 0; t < m; t++) {
@@ -673,6 +684,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       const double nx1 = ROT ? x1 + a12 * x2 : x1 + a12 * x2 + b10 * u0 + c1;
       const double nx2 = x2 + b20 * u0 + b21 * u1 + c2;
       x0 = nx0; x1 = nx1; x2 = nx2;
+      if constexpr (SCR) {
+        const double wx = (ROT ? cs * x0 - sn * x1 : x0) + X0, wy = (ROT ? sn * x0 + cs * x1 : x1) + Y0;
+        const double ta0 = ga0 * wx, tb0 = gb0 * wy, ta1 = ga1 * wx, tb1 = gb1 * wy;
+        gok = gok & (ta0 + tb0 + gc0 >= 1e-6 * (1.0 + fabs(ta0) + fabs(tb0) + fabs(gc0))) &
+              (ta1 + tb1 + gc1 >= 1e-6 * (1.0 + fabs(ta1) + fabs(tb1) + fabs(gc1)));
+      }
       if (owner) {
         uo[2 * i] = solved ? (float)u0 : nanv;
         uo[2 * i + 1] = solved ? (float)u1 : nanv;
@@ -694,6 +711,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     const double dnan = __longlong_as_double(0x7ff8000000000000ll);
     if (qowner && oo.cost) oo.cost[b] = solved ? J : dnan;
     if (qowner && oo.obj) oo.obj[b] = solved ? J - Cr - Cu : dnan;
+  }
+  if constexpr (SCR) {
+    const bool qfail = (fold(__ballot(!gok)) >> sl) & 1ull;
+    const bool ok0 = (ga0 * X0 + gb0 * Y0 >= -gc0 - 1e-9) & (ga1 * X0 + gb1 * Y0 >= -gc1 - 1e-9);
+    if (qowner && (qfail || !ok0 || !solved)) oo.scr_list[atomicAdd(oo.scr_count, 1)] = b;
   }
   if (qowner) {
     status_out[b] = bad ? F110QP_NUMERICAL_ID : (done ? F110QP_SOLVED_ID : F110QP_MAX_ITER_ID);
@@ -756,7 +778,7 @@ inline int seg_scratch_mode(const KParams& P, int B, int S, const LaneWork& lw) 
   return f64 ? 1 : (f32 ? 2 : 0);
 }
 
-template <int S, bool ROT>
+template <int S, bool ROT, bool SCR>
 hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                              float* uo, float* xo, int* st, int* its, const WarmState& ws,
                              const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
@@ -778,9 +800,9 @@ hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const flo
                        lw.kmax, oo);
     return hipGetLastError();
   };
-  if (mode == 2) return go(&lane_seg_kernel<S, ROT, false, float>, seg_lds_bytes(P.N, S, false, true));
-  return fst ? go(&lane_seg_kernel<S, ROT, true>, seg_lds_bytes(P.N, S, true))
-             : go(&lane_seg_kernel<S, ROT, false>, seg_lds_bytes(P.N, S, false));
+  if (mode == 2) return go(&lane_seg_kernel<S, ROT, false, float, SCR>, seg_lds_bytes(P.N, S, false, true));
+  return fst ? go(&lane_seg_kernel<S, ROT, true, double, SCR>, seg_lds_bytes(P.N, S, true))
+             : go(&lane_seg_kernel<S, ROT, false, double, SCR>, seg_lds_bytes(P.N, S, false));
 }
 
 }  // namespace f110qp

@@ -218,6 +218,24 @@ def test_segments_fp32_degenerate_bound(oracle, capi, monkeypatch, kmax):
         assert (st == capi.SOLVED).all(), (q, np.unique(st, return_counts=True))
 
 
+def test_c4_32768_per_gpu_two_rounds(oracle, capi):
+    """65,536 over 2 GPUs: 32,768 x N = 40 per GPU on the segmented kernel at S = 4 with fp32
+    scratch in two dispatch rounds (2,048 waves, four resident per CU by LDS). Parity on a
+    strided sample that covers both rounds plus the scenario at the round boundary."""
+    N, B = 40, 32768
+    g = workload.make_grouped_batch(274, N, seed=4044)
+    w = {k: np.ascontiguousarray(g[k][:B]) for k in ("x0", "u_lin", "x_ref")}
+    s = capi.Solver(capi.default_config(N))
+    assert s.lane_segments(B) == 4 and s.backend_info(B)[2] == 2
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+    s.close()
+    assert (st == capi.SOLVED).all()
+    idx = np.concatenate([np.arange(0, B, 41), np.arange(16320, 16440)])
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
+    assert (sr == oracle.SOLVED).all()
+    assert rel_err(u[idx], ur).max() <= 2e-6 and rel_err(x[idx], xr).max() <= 2e-6
+
+
 def test_c4_16384_per_gpu_auto(oracle, capi):
     """The middle of the C4 strong-scaling curve: 16,384 x N = 40 QPs per GPU (65,536 over 4
     GPUs). AUTO runs the segmented kernel at S = 4 on fp32 scratch (fp64 does not fit four waves
