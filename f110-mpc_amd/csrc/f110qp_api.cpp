@@ -97,7 +97,7 @@ struct f110qp_ctx {
   DevBuf gW, gkey, glead;    // grouped mode: W = H^-1, key and leader per group
   DevBuf dgrp;               // host-pointer grouped calls: device copy of the group ids
   DevBuf lscr;               // lane back end: HBM Riccati scratch (when not in LDS)
-  DevBuf hand;               // gap rows: two counts + one list (B + 2 ints; LaneWork::hand)
+  DevBuf hand;               // gap rows: two counts, one list, the screen priorities (2B + 2 ints)
   f110qp::IpmKnobs ipm;      // lane back end, gap rows: interior-point knobs (test/bench hooks)
   int lane_kmax = 16;        // lane back end: PDAS passes before single (least-index) flips
   int lane_mode = 0;         // lane scratch placement (LaneWork::mode)
@@ -227,6 +227,10 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
   // test hook: F110QP_LANE_SEG_F32=1 forces the segmented kernel's float references and scratch
   if (const char* ef = std::getenv("F110QP_LANE_SEG_F32")) c->lane_seg32 = std::atoi(ef) != 0;
   if (const char* eg = std::getenv("F110QP_GAP_SCREEN")) c->gap_screen = std::atoi(eg) != 0;
+  if (const char* ep = std::getenv("F110QP_LANE_PASSCAP")) {  // measurement: passes per lane launch
+    const int v = std::atoi(ep);
+    if (v > 0 && v < 1000) c->kp.pass_cap = v;
+  }
   // test hook: F110QP_PDAS_MAX caps the wave kernel's box PDAS passes (0 = GI from scratch)
   k.pdas_max = 10;
   if (const char* ep = std::getenv("F110QP_PDAS_MAX")) {
@@ -337,7 +341,7 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) {
     // count + list of the interior point's hand-over (lane back end) or of the fp64 re-check of
     // the wave kernel's non-SOLVED QPs (wave back end)
-    if ((e = c->hand.ensure(((size_t)batch + 2) * sizeof(int))) != hipSuccess)
+    if ((e = c->hand.ensure((2 * (size_t)batch + 2) * sizeof(int))) != hipSuccess)
       return hip_fail(e, "hipMalloc hand-over list");
     lw->hand = (int*)c->hand.p;
     lw->screen = *backend == f110qp::BACKEND_WAVE && gap_screen(c, batch, grouped);

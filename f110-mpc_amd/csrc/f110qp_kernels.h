@@ -24,6 +24,7 @@ struct KParams {
   int max_iter;   // active-set iteration cap
   int xr_stride;  // points per QP in x_ref (>= N; the reference passes its whole miniPath)
   int pdas_max;   // PDAS passes of the wave kernel's box path before its GI loop takes over
+  int pass_cap = 0;  // lane kernels: passes per launch (0: max_iter; measurement knob F110QP_LANE_PASSCAP)
 };
 
 // Warm-start state of a context (all null = cold solve). Per QP slot b of the batch:
@@ -70,6 +71,7 @@ struct LaneWork {
   int seg32 = 0;  // segmented kernel: 1 forces float references and Riccati scratch in LDS
   int* hand = nullptr;  // gap rows: two counts (hand[0]: hand-over / screen, hand[1]: the fp64
                         // re-check) + one list (hand + 2, B ints) the two use one after the other
+                        // + the screen's per-QP priorities (hand + 2 + B, B ints)
   int screen = 0;       // gap rows, wave back end: box solve on the lane kernel first, GI only
                         // for the QPs whose box optimum violates a gap row (f110qp_kernels.hip)
   IpmKnobs ipm;
@@ -83,10 +85,10 @@ struct ObjOut {
   double* obj = nullptr;
   double* cost = nullptr;
   // gap-row box screen fused into the segmented lane kernel's output sweep (f110qp_kernels.hip):
-  // the half-spaces, and the count + list the QPs that need GI are appended to (null: no screen)
+  // the half-spaces, and per QP the GI priority it writes (0: the box optimum stands; else 1 + the
+  // gap rows it violates; null: no screen)
   const float* scr_hs = nullptr;
-  int* scr_count = nullptr;
-  int* scr_list = nullptr;
+  int* scr_prio = nullptr;
 };
 
 // waves the lane kernel's grid aims for (one per CU of the MI355X's 256)

@@ -41,34 +41,70 @@ constexpr int kHandGrid = 256;
 // Gap-row screen after a box-only lane solve: a QP whose box optimum keeps every gap row of stages
 // 1..N strictly satisfied has that point as its optimum with the gap rows (adding constraints that
 // hold at the unique minimiser of a strictly convex QP does not move it), so its lane outputs stand.
-// Every other QP goes on the list for the wave kernel's GI: a gap row violated or within the
-// margin, the stage-0 rows violated (constant rows, x0 on both lines by constraints.cpp:233-246;
-// violated, the wedge is infeasible), a non-SOLVED
-// box status, non-finite values. The margin is 1e-6 of the row's terms: ~8x the float rounding of
-// the stored x (absolute coordinates) plus the row's float data.
+// Every other QP goes to the wave kernel's GI: a gap row violated or within the margin, the stage-0
+// rows violated (constant rows, x0 on both lines by constraints.cpp:233-246; violated, the wedge is
+// infeasible), a non-SOLVED box status, non-finite values. The margin is 1e-6 of the row's terms:
+// ~8x the float rounding of the stored x (absolute coordinates) plus the row's float data. This
+// kernel serves the sequential lane kernel's batches (from stored float x); the segmented kernel
+// evaluates the same test in its output sweep, in fp64. Output: the GI priority of each QP (0: the
+// box optimum stands, else 1 + the violated rows; 1 for the stage-0 / status cases).
 __global__ __launch_bounds__(256) void gap_screen_kernel(const int B, const int N,
                                                          const float* __restrict__ x0g,
                                                          const float* __restrict__ hsg,
                                                          const float* __restrict__ xo,
                                                          const int* __restrict__ status,
-                                                         int* __restrict__ count, int* __restrict__ list) {
+                                                         int* __restrict__ prio) {
   const int b = blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
-  bool ok = status[b] == F110QP_SOLVED_ID;
   const double px = (double)x0g[3 * b], py = (double)x0g[3 * b + 1];
   const float* xb = xo + (size_t)b * (N + 1) * 3;
+  bool ok0 = status[b] == F110QP_SOLVED_ID;
+  int nv = 0;
 #pragma unroll
   for (int h = 0; h < 2; h++) {
     const double a = (double)hsg[6 * b + 3 * h], bb = (double)hsg[6 * b + 3 * h + 1],
                  c = (double)hsg[6 * b + 3 * h + 2];
-    ok = ok && (a * px + bb * py >= -c - 1e-9);  // stage 0: constant rows
-    for (int i = 1; i <= N && ok; i++) {
+    ok0 = ok0 && (a * px + bb * py >= -c - 1e-9);  // stage 0: constant rows
+    for (int i = 1; i <= N; i++) {
       const double x = (double)xb[3 * i], y = (double)xb[3 * i + 1];
       const double ax = a * x, by = bb * y;
-      ok = (ax + by + c >= 1e-6 * (1.0 + fabs(ax) + fabs(by) + fabs(c)));
+      nv += !(ax + by + c >= 1e-6 * (1.0 + fabs(ax) + fabs(by) + fabs(c)));
     }
   }
-  if (!ok) list[atomicAdd(count, 1)] = b;
+  prio[b] = !ok0 ? 1 : (nv > 0 ? 1 + nv : 0);
+}
+
+// The GI list in priority order, heavy first (one workgroup; a counting sort over the priorities
+// 1..kPrioMax by LDS histogram, scan and scatter): a QP's GI chain grows with the gap rows its box
+// optimum violates, and a long chain that starts late in the dispatch adds its whole length to
+// the launch (an atomic append in the lane kernel's wave completion order put them late; same-box
+// A/B on C3: step 236-242 -> 225 us with this order).
+constexpr int kPrioMax = 127;
+__global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int* __restrict__ prio,
+                                                         int* __restrict__ count, int* __restrict__ list) {
+  __shared__ int hist[kPrioMax + 1];
+  __shared__ int off[kPrioMax + 1];
+  const int t = threadIdx.x;
+  if (t <= kPrioMax) hist[t] = 0;
+  __syncthreads();
+  for (int b = t; b < B; b += 1024) {
+    const int p = min(prio[b], kPrioMax);
+    if (p > 0) atomicAdd(&hist[p], 1);
+  }
+  __syncthreads();
+  if (t == 0) {  // descending exclusive offsets: the highest priority first
+    int run = 0;
+    for (int p = kPrioMax; p >= 1; p--) {
+      off[p] = run;
+      run += hist[p];
+    }
+    *count = run;
+  }
+  __syncthreads();
+  for (int b = t; b < B; b += 1024) {
+    const int p = min(prio[b], kPrioMax);
+    if (p > 0) list[atomicAdd(&off[p], 1)] = b;
+  }
 }
 
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
@@ -86,25 +122,27 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
                           lw.hand, B < kHandGrid ? B : kHandGrid, oo, s);
   }
   if (hs && lw.screen) {
-    // one memset clears both counts (screen hand[0], re-check hand[1]); the box-only lane solve of
-    // every QP (the segmented kernel evaluates the screen in its output sweep, in fp64, and lists
-    // the QPs that need GI; the sequential kernel leaves it to gap_screen_kernel), GI over the
-    // list (grid B: the waves past the device-side count exit at once), the fp64 re-check
-    hipError_t e = hipMemsetAsync(lw.hand, 0, 2 * sizeof(int), s);
+    // the box-only lane solve of every QP (the segmented kernel evaluates the screen in its output
+    // sweep, in fp64, and writes each QP's GI priority; the sequential kernel leaves it to
+    // gap_screen_kernel), the GI list heavy first (gap_order_kernel writes count hand[0] and the
+    // list), GI over it (grid B: the waves past the device-side count exit at once), the fp64
+    // re-check (count hand[1], cleared by the one memset)
+    hipError_t e = hipMemsetAsync(lw.hand + 1, 0, sizeof(int), s);  // the re-check count
     if (e != hipSuccess) return e;
+    int* prio = lw.hand + 2 + B;
     const bool fused = lane_segments(P, B, lw) > 1;
     ObjOut so = oo;
     if (fused) {
       so.scr_hs = hs;
-      so.scr_count = lw.hand;
-      so.scr_list = lw.hand + 2;
+      so.scr_prio = prio;
     }
     if ((e = launch_lane(P, B, x0, ul, xr, uo, xo, st, its, WarmState(), lw, so, s)) != hipSuccess) return e;
     if (!fused) {
-      hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st,
-                         lw.hand, lw.hand + 2);
+      hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st, prio);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    hipLaunchKernelGGL(gap_order_kernel, dim3(1), dim3(1024), 0, s, B, prio, lw.hand, lw.hand + 2);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 2,
                        lw.hand, B, oo, s);
     if (e != hipSuccess) return e;

@@ -334,7 +334,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
   // one flip per pass, the least-index rule). No change certifies the KKT conditions and the
   // u_i the forward sweep left in the scratch are the solution; a converged lane's further
   // sweeps reproduce them exactly.
-  const int max_pass = P.max_iter > kmax ? P.max_iter : kmax;
+  const int max_pass = P.pass_cap > 0 ? P.pass_cap : (P.max_iter > kmax ? P.max_iter : kmax);
   for (int pass = 0; pass < max_pass; pass++) {
     if (__ballot(!done) == 0ull) break;
     const bool single = pass >= kmax;

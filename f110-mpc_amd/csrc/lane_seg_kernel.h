@@ -281,7 +281,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   double xs0 = 0.0, xs1 = 0.0, xs2 = 0.0, lm0 = 0.0, lm1 = 0.0, lm2 = 0.0;
 
 
-  const int max_pass = P.max_iter > kmax ? P.max_iter : kmax;
+  const int max_pass = P.pass_cap > 0 ? P.pass_cap : (P.max_iter > kmax ? P.max_iter : kmax);
 #ifdef F110QP_STAMPS
   t_setup = __builtin_amdgcn_s_memtime() - t_start;
 #endif
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     const float* h6 = oo.scr_hs + 6 * (size_t)b;
     ga0 = h6[0]; gb0 = h6[1]; gc0 = h6[2]; ga1 = h6[3]; gb1 = h6[4]; gc1 = h6[5];
   }
-  bool gok = true;
+  int nviol = 0;  // gap rows of this lane's stages the box optimum violates (or within the margin)
   {
     double x0 = xs0, x1 = xs1, x2 = xs2;
     for (int t = 0; t < m; t++) {
@@ -687,8 +687,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       if constexpr (SCR) {
         const double wx = (ROT ? cs * x0 - sn * x1 : x0) + X0, wy = (ROT ? sn * x0 + cs * x1 : x1) + Y0;
         const double ta0 = ga0 * wx, tb0 = gb0 * wy, ta1 = ga1 * wx, tb1 = gb1 * wy;
-        gok = gok & (ta0 + tb0 + gc0 >= 1e-6 * (1.0 + fabs(ta0) + fabs(tb0) + fabs(gc0))) &
-              (ta1 + tb1 + gc1 >= 1e-6 * (1.0 + fabs(ta1) + fabs(tb1) + fabs(gc1)));
+        nviol += !(ta0 + tb0 + gc0 >= 1e-6 * (1.0 + fabs(ta0) + fabs(tb0) + fabs(gc0)));
+        nviol += !(ta1 + tb1 + gc1 >= 1e-6 * (1.0 + fabs(ta1) + fabs(tb1) + fabs(gc1)));
       }
       if (owner) {
         uo[2 * i] = solved ? (float)u0 : nanv;
@@ -713,9 +713,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     if (qowner && oo.obj) oo.obj[b] = solved ? J - Cr - Cu : dnan;
   }
   if constexpr (SCR) {
-    const bool qfail = (fold(__ballot(!gok)) >> sl) & 1ull;
+    // the QP's violation count over its S lanes; GI priority 1 + count (the list is ordered by it,
+    // heavy first: gap_order_kernel), 1 for a violated stage-0 row or a box solve that failed
+#pragma unroll
+    for (int k = L; k < 64; k <<= 1) nviol += __shfl_xor(nviol, k, 64);
     const bool ok0 = (ga0 * X0 + gb0 * Y0 >= -gc0 - 1e-9) & (ga1 * X0 + gb1 * Y0 >= -gc1 - 1e-9);
-    if (qowner && (qfail || !ok0 || !solved)) oo.scr_list[atomicAdd(oo.scr_count, 1)] = b;
+    if (qowner) oo.scr_prio[b] = (!solved || !ok0) ? 1 : (nviol > 0 ? 1 + nviol : 0);
   }
   if (qowner) {
     status_out[b] = bad ? F110QP_NUMERICAL_ID : (done ? F110QP_SOLVED_ID : F110QP_MAX_ITER_ID);
