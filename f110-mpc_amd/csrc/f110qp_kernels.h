@@ -89,6 +89,10 @@ struct ObjOut {
   // gap rows it violates; null: no screen)
   const float* scr_hs = nullptr;
   int* scr_prio = nullptr;
+  // wave kernel, gap rows: QPs it does not report SOLVED are appended here for the fp64 re-check
+  // (count + list; null: the re-check flags them itself)
+  int* rc_count = nullptr;
+  int* rc_list = nullptr;
 };
 
 // waves the lane kernel's grid aims for (one per CU of the MI355X's 256)
@@ -116,11 +120,12 @@ hipError_t launch_lane_ipm(const KParams& P, int B, const float* x0, const float
 // fp64 re-check of the wave kernel's gap-row QPs it did not report SOLVED (lane_ipm_inst.hip):
 // the interior point over their list; polished -> SOLVED, Farkas certificate -> PRIMAL_INFEASIBLE,
 // else the wave kernel's answer stands. Needs lw.hand (B + 2 ints; count hand[1], zeroed by the
-// caller when `zeroed`).
+// caller when `zeroed`; `flagged`: the wave kernel already appended its non-SOLVED QPs to this
+// list, count hand[1]).
 hipError_t launch_gap_recheck(const KParams& P, int B, const float* x0, const float* u_lin,
                               const float* x_ref, const float* hs, float* u_out, float* x_out,
                               int* status, int* iters, const LaneWork& lw, const ObjOut& oo,
-                              hipStream_t stream, bool zeroed = false);
+                              hipStream_t stream, bool zeroed = false, const int* flagged = nullptr);
 
 enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
 

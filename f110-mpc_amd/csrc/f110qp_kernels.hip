@@ -81,7 +81,8 @@ __global__ __launch_bounds__(256) void gap_screen_kernel(const int B, const int 
 // A/B on C3: step 236-242 -> 225 us with this order).
 constexpr int kPrioMax = 127;
 __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int* __restrict__ prio,
-                                                         int* __restrict__ count, int* __restrict__ list) {
+                                                         int* __restrict__ count, int* __restrict__ list,
+                                                         int* __restrict__ zero) {
   __shared__ int hist[kPrioMax + 1];
   __shared__ int off[kPrioMax + 1];
   const int t = threadIdx.x;
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int*
       run += hist[p];
     }
     *count = run;
+    *zero = 0;  // the re-check count the GI kernel appends to next
   }
   __syncthreads();
   for (int b = t; b < B; b += 1024) {
@@ -127,8 +129,7 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
     // gap_screen_kernel), the GI list heavy first (gap_order_kernel writes count hand[0] and the
     // list), GI over it (grid B: the waves past the device-side count exit at once), the fp64
     // re-check (count hand[1], cleared by the one memset)
-    hipError_t e = hipMemsetAsync(lw.hand + 1, 0, sizeof(int), s);  // the re-check count
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
     int* prio = lw.hand + 2 + B;
     const bool fused = lane_segments(P, B, lw) > 1;
     ObjOut so = oo;
@@ -141,12 +142,17 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
       hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st, prio);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(gap_order_kernel, dim3(1), dim3(1024), 0, s, B, prio, lw.hand, lw.hand + 2);
+    hipLaunchKernelGGL(gap_order_kernel, dim3(1), dim3(1024), 0, s, B, prio, lw.hand, lw.hand + 2, lw.hand + 1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    // GI appends its non-SOLVED QPs for the re-check (count hand[1], zeroed by the order kernel)
+    // into the priority array, dead once the order kernel ran (hand + 2 holds the list GI reads)
+    ObjOut go = oo;
+    go.rc_count = lw.hand + 1;
+    go.rc_list = prio;
     e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 2,
-                       lw.hand, B, oo, s);
+                       lw.hand, B, go, s);
     if (e != hipSuccess) return e;
-    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s, true);
+    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s, true, prio);
   }
   if (hs) {
     hipError_t e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,

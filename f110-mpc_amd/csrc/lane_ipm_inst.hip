@@ -64,7 +64,7 @@ hipError_t launch_lane_ipm(const KParams& P, int B, const float* x0, const float
 constexpr int kRecheckCap = 4096;
 hipError_t launch_gap_recheck(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                               const float* hs, float* uo, float* xo, int* st, int* its, const LaneWork& lw,
-                              const ObjOut& oo, hipStream_t s, bool zeroed) {
+                              const ObjOut& oo, hipStream_t s, bool zeroed, const int* flagged) {
   if (B <= 0 || !lw.hand) return hipSuccess;
   const int cap = B < kRecheckCap ? B : kRecheckCap;
   LaneWork l2 = lw;
@@ -72,15 +72,18 @@ hipError_t launch_gap_recheck(const KParams& P, int B, const float* x0, const fl
   const int S = lane_ipm_segments(P, cap, l2);
   if (S == 0) return hipSuccess;  // no segmentation fits this horizon: the wave kernel's answer stands
   hipError_t e = hipSuccess;
-  if (!zeroed && (e = hipMemsetAsync(lw.hand + 1, 0, sizeof(int), s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(ipm_flag_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, st, lw.hand + 1, lw.hand + 2);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const int* list = flagged ? flagged : lw.hand + 2;
+  if (!flagged) {
+    if (!zeroed && (e = hipMemsetAsync(lw.hand + 1, 0, sizeof(int), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(ipm_flag_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, st, lw.hand + 1, lw.hand + 2);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   const bool rot = lw.rot && P.q[0] == P.q[1];
   // grid of `cap` QPs; the kernel reads the count and idle waves exit at once
   return rot ? ipm_s<true>(S, P, cap, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, lw.ipm, oo, s,
-                           lw.hand + 2, lw.hand + 1, 1)
+                           list, lw.hand + 1, 1)
              : ipm_s<false>(S, P, cap, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, lw.ipm, oo, s,
-                            lw.hand + 2, lw.hand + 1, 1);
+                            list, lw.hand + 1, 1);
 }
 
 }  // namespace f110qp

@@ -1906,6 +1906,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   if (lane == 0) {
     status_out[b] = status;
     if (iters_out) iters_out[b] = it;
+    if (oo.rc_list && status != F110QP_SOLVED_ID) oo.rc_list[atomicAdd(oo.rc_count, 1)] = b;  // re-check
   }
   if (ws.act != nullptr && !grp && Hdbg == nullptr) {
 #pragma unroll
