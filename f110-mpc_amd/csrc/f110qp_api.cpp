@@ -107,6 +107,9 @@ struct f110qp_ctx {
   int lane_seg = 0;          // lane horizon segments per QP (LaneWork::seg: 0 auto, 1 off, 2/4/8)
   int lane_seg32 = 0;        // segmented kernel: force fp32 references + scratch (LaneWork::seg32)
   int gap_screen = -1;      // gap rows, AUTO: box screen on the lane kernel (-1 by batch, 0 off, 1 on)
+  int gap_early = 256;      // screen: predicted-heaviest QPs whose GI starts with the box solve
+  hipStream_t aux = nullptr;             // second stream of the screen path (highest priority)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipStream_t stream = nullptr;
 };
 
@@ -227,6 +230,10 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
   // test hook: F110QP_LANE_SEG_F32=1 forces the segmented kernel's float references and scratch
   if (const char* ef = std::getenv("F110QP_LANE_SEG_F32")) c->lane_seg32 = std::atoi(ef) != 0;
   if (const char* eg = std::getenv("F110QP_GAP_SCREEN")) c->gap_screen = std::atoi(eg) != 0;
+  if (const char* ee = std::getenv("F110QP_GAP_EARLY")) {  // 0: no early GI
+    const int v = std::atoi(ee);
+    if (v >= 0 && v <= (1 << 20)) c->gap_early = v;
+  }
   if (const char* ep = std::getenv("F110QP_LANE_PASSCAP")) {  // measurement: passes per lane launch
     const int v = std::atoi(ep);
     if (v > 0 && v < 1000) c->kp.pass_cap = v;
@@ -252,6 +259,9 @@ void f110qp_destroy(f110qp_ctx* c) {
   c->hand.release();
   c->gW.release(); c->gkey.release(); c->glead.release(); c->dgrp.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   delete c;
 }
 
@@ -341,11 +351,27 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) {
     // count + list of the interior point's hand-over (lane back end) or of the fp64 re-check of
     // the wave kernel's non-SOLVED QPs (wave back end)
-    if ((e = c->hand.ensure((2 * (size_t)batch + 2) * sizeof(int))) != hipSuccess)
+    if ((e = c->hand.ensure((5 * (size_t)batch + 4) * sizeof(int))) != hipSuccess)  // f110qp::HandLayout
       return hip_fail(e, "hipMalloc hand-over list");
     lw->hand = (int*)c->hand.p;
     lw->screen = *backend == f110qp::BACKEND_WAVE && gap_screen(c, batch, grouped);
     if (!lw->screen) return F110QP_OK;
+    if (c->gap_early > 0) {  // the early GI's stream and events (created once, on the current device)
+      if (!c->aux) {
+        int lo = 0, hi = 0;
+        if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess ||
+            (e = hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, hi)) != hipSuccess)
+          return hip_fail(e, "hipStreamCreate (screen aux stream)");
+      }
+      if (!c->ev_fork && (e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e, "hipEventCreate");
+      if (!c->ev_join && (e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e, "hipEventCreate");
+      lw->early = c->gap_early;
+      lw->aux = c->aux;
+      lw->ev_fork = c->ev_fork;
+      lw->ev_join = c->ev_join;
+    }
   } else if (*backend == f110qp::BACKEND_WAVE) {
     return F110QP_OK;
   }

@@ -58,6 +58,21 @@ struct IpmKnobs {
   int debug = 0;         // test hook: return every QP's current iterate as SOLVED (no polish test)
 };
 
+// LaneWork::hand for a call of B gap-row QPs: four counts, then five B-int arrays.
+struct HandLayout {
+  int* c_list;   // [0] GI list count (hand-over of the interior point, or the screen's GI list)
+  int* c_rc;     // [1] the fp64 re-check's count
+  int* c_early;  // [2] the early GI list's count
+  int* list;     // GI list (hand-over / screen), and the re-check list of the flag kernel
+  int* prio;     // screen: GI priority per QP
+  int* rc;       // re-check list the GI kernel appends to
+  int* mark;     // early: 1 for the QPs GI takes on the aux stream
+  int* elist;    // early GI list
+  HandLayout(int* h, int B)
+      : c_list(h), c_rc(h + 1), c_early(h + 2), list(h + 4), prio(h + 4 + (size_t)B),
+        rc(h + 4 + 2 * (size_t)B), mark(h + 4 + 3 * (size_t)B), elist(h + 4 + 4 * (size_t)B) {}
+};
+
 // Workspace of the lane-per-QP kernel (lane_kernel.h): the HBM Riccati scratch when it does
 // not stay in LDS (ceil(B/L) x N x 8 x L doubles at most, L QPs per wave <= 64).
 struct LaneWork {
@@ -69,11 +84,13 @@ struct LaneWork {
   int dref = 1;   // 1: fp64 references in LDS when the resident waves fit (DREF); 0: float
   int seg = 0;    // horizon segments per QP (lane_seg_kernel.h): 0 auto, 1 off, 2 / 4 / 8 forced
   int seg32 = 0;  // segmented kernel: 1 forces float references and Riccati scratch in LDS
-  int* hand = nullptr;  // gap rows: two counts (hand[0]: hand-over / screen, hand[1]: the fp64
-                        // re-check) + one list (hand + 2, B ints) the two use one after the other
-                        // + the screen's per-QP priorities (hand + 2 + B, B ints)
+  int* hand = nullptr;  // gap rows: counts + per-QP lists, layout HandLayout below (5 B + 4 ints)
   int screen = 0;       // gap rows, wave back end: box solve on the lane kernel first, GI only
                         // for the QPs whose box optimum violates a gap row (f110qp_kernels.hip)
+  int early = 0;        // screen: GI for up to this many predicted-heavy QPs on the aux stream,
+                        // concurrently with the box solve (0: off)
+  hipStream_t aux = nullptr;  // the context's second stream and its fork / join events
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   IpmKnobs ipm;
 };
 
@@ -89,6 +106,7 @@ struct ObjOut {
   // gap rows it violates; null: no screen)
   const float* scr_hs = nullptr;
   int* scr_prio = nullptr;
+  const int* scr_skip = nullptr;  // QPs the early GI owns: no outputs from the box solve
   // wave kernel, gap rows: QPs it does not report SOLVED are appended here for the fp64 re-check
   // (count + list; null: the re-check flags them itself)
   int* rc_count = nullptr;

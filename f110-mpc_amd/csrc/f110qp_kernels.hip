@@ -100,12 +100,71 @@ __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int*
       run += hist[p];
     }
     *count = run;
-    *zero = 0;  // the re-check count the GI kernel appends to next
+    if (zero) *zero = 0;  // the re-check count the GI kernel appends to next
   }
   __syncthreads();
   for (int b = t; b < B; b += 1024) {
     const int p = min(prio[b], kPrioMax);
     if (p > 0) list[atomicAdd(&off[p], 1)] = b;
+  }
+}
+
+// Early GI (screen path): the QPs predicted heaviest for GI start on the aux stream while the
+// box solve runs, so the longest chains no longer wait for it. The predictor, per QP: the stages
+// i = 1..N at which the free motion from x0 at the linearisation speed (x0 + v dt i (cos th0,
+// sin th0)) leaves the gap wedge, summed over both rows (numpy model on the C3 batch: the top
+// 128 by this count hold the 10 heaviest QPs for GI, 23 of the 40 heaviest). One workgroup: LDS
+// histogram, descending scan, the first K into the early list with mark[b] = 1; the re-check
+// count is cleared here, before the fork, for the two GI launches that append to it.
+__global__ __launch_bounds__(1024) void gap_presort_kernel(const int B, const int N, const float dt,
+                                                           const float* __restrict__ x0g,
+                                                           const float* __restrict__ ulg,
+                                                           const float* __restrict__ hsg, const int K,
+                                                           int* __restrict__ mark, int* __restrict__ elist,
+                                                           int* __restrict__ ecount, int* __restrict__ rc_count) {
+  __shared__ int hist[kPrioMax + 1];
+  __shared__ int off[kPrioMax + 1];
+  const int t = threadIdx.x;
+  if (t <= kPrioMax) hist[t] = 0;
+  __syncthreads();
+  auto proxy = [&](int b) {
+    const double X = (double)x0g[3 * b], Y = (double)x0g[3 * b + 1], th = (double)x0g[3 * b + 2];
+    const double step = (double)ulg[2 * b] * (double)dt;
+    const double cx = step * cos(th), cy = step * sin(th);
+    const float* h6 = hsg + 6 * (size_t)b;
+    const double a0 = h6[0], b0 = h6[1], c0 = h6[2], a1 = h6[3], b1 = h6[4], c1 = h6[5];
+    int n = 0;
+    for (int i = 1; i <= N; i++) {
+      const double x = X + cx * i, y = Y + cy * i;
+      n += (a0 * x + b0 * y + c0 < 0.0) + (a1 * x + b1 * y + c1 < 0.0);
+    }
+    return min(n, kPrioMax);
+  };
+  for (int b = t; b < B; b += 1024) {
+    const int p = proxy(b);
+    mark[b] = 0;
+    if (p > 0) atomicAdd(&hist[p], 1);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int run = 0;
+    for (int p = kPrioMax; p >= 1; p--) {
+      off[p] = run;
+      run += hist[p];
+    }
+    *ecount = min(run, K);
+    *rc_count = 0;
+  }
+  __syncthreads();
+  for (int b = t; b < B; b += 1024) {
+    const int p = proxy(b);
+    if (p > 0) {
+      const int pos = atomicAdd(&off[p], 1);
+      if (pos < K) {
+        elist[pos] = b;
+        mark[b] = 1;
+      }
+    }
   }
 }
 
@@ -117,42 +176,58 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
   if (hs && backend == BACKEND_LANE) {
     // interior point on the lane back end, then the wave kernel's GI over the QPs it handed over
     // (none in the common case: every wave of that launch reads the zero count and exits)
-    hipError_t e = hipMemsetAsync(lw.hand, 0, sizeof(int), s);
+    const HandLayout H(lw.hand, B);
+    hipError_t e = hipMemsetAsync(H.c_list, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
     if ((e = launch_lane_ipm(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s)) != hipSuccess) return e;
-    return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 2,
-                          lw.hand, B < kHandGrid ? B : kHandGrid, oo, s);
+    return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), H.list,
+                          H.c_list, B < kHandGrid ? B : kHandGrid, oo, s);
   }
   if (hs && lw.screen) {
-    // the box-only lane solve of every QP (the segmented kernel evaluates the screen in its output
+    // The box-only lane solve of every QP (the segmented kernel evaluates the screen in its output
     // sweep, in fp64, and writes each QP's GI priority; the sequential kernel leaves it to
-    // gap_screen_kernel), the GI list heavy first (gap_order_kernel writes count hand[0] and the
-    // list), GI over it (grid B: the waves past the device-side count exit at once), the fp64
-    // re-check (count hand[1], cleared by the one memset)
+    // gap_screen_kernel), the GI list heavy first (gap_order_kernel), GI over it (grid B: the waves
+    // past the device-side count exit at once), the fp64 re-check of what GI did not solve (the GI
+    // kernel appends those itself). With the segmented kernel and lw.early, the predicted-heaviest
+    // QPs go to GI first, on the aux stream, concurrently with the box solve, which skips them.
+    const HandLayout H(lw.hand, B);
     hipError_t e = hipSuccess;
-    int* prio = lw.hand + 2 + B;
     const bool fused = lane_segments(P, B, lw) > 1;
+    const bool early = fused && lw.early > 0 && lw.aux && lw.ev_fork && lw.ev_join;
+    ObjOut go = oo;  // GI: non-SOLVED QPs appended for the re-check
+    go.rc_count = H.c_rc;
+    go.rc_list = H.rc;
+    if (early) {
+      const int K = lw.early < B ? lw.early : B;
+      hipLaunchKernelGGL(gap_presort_kernel, dim3(1), dim3(1024), 0, s, B, P.N, P.dt, x0, ul, hs, K, H.mark,
+                         H.elist, H.c_early, H.c_rc);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      if ((e = hipEventRecord(lw.ev_fork, s)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(lw.aux, lw.ev_fork, 0)) != hipSuccess) return e;
+      e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), H.elist, H.c_early,
+                         K, go, lw.aux);
+      if (e != hipSuccess) return e;
+      if ((e = hipEventRecord(lw.ev_join, lw.aux)) != hipSuccess) return e;
+    }
     ObjOut so = oo;
     if (fused) {
       so.scr_hs = hs;
-      so.scr_prio = prio;
+      so.scr_prio = H.prio;
+      so.scr_skip = early ? H.mark : nullptr;
     }
     if ((e = launch_lane(P, B, x0, ul, xr, uo, xo, st, its, WarmState(), lw, so, s)) != hipSuccess) return e;
     if (!fused) {
-      hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st, prio);
+      hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st, H.prio);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(gap_order_kernel, dim3(1), dim3(1024), 0, s, B, prio, lw.hand, lw.hand + 2, lw.hand + 1);
+    hipLaunchKernelGGL(gap_order_kernel, dim3(1), dim3(1024), 0, s, B, H.prio, H.c_list, H.list,
+                       early ? nullptr : H.c_rc);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    // GI appends its non-SOLVED QPs for the re-check (count hand[1], zeroed by the order kernel)
-    // into the priority array, dead once the order kernel ran (hand + 2 holds the list GI reads)
-    ObjOut go = oo;
-    go.rc_count = lw.hand + 1;
-    go.rc_list = prio;
-    e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), lw.hand + 2,
-                       lw.hand, B, go, s);
+    e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), H.list, H.c_list, B,
+                       go, s);
     if (e != hipSuccess) return e;
-    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s, true, prio);
+    if (early && (e = hipStreamWaitEvent(s, lw.ev_join, 0)) != hipSuccess) return e;
+    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s, true, H.rc);
   }
   if (hs) {
     hipError_t e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,

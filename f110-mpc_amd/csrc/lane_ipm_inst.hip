@@ -50,17 +50,18 @@ hipError_t launch_lane_ipm(const KParams& P, int B, const float* x0, const float
   if (B <= 0) return hipSuccess;
   const bool rot = lw.rot && P.q[0] == P.q[1];
   const int S = lane_ipm_segments(P, B, lw);
-  return rot ? ipm_s<true>(S, P, B, x0, ul, xr, hs, uo, xo, st, its, lw.hand + 2, lw.hand, lw.ipm, oo, s, nullptr,
+  const HandLayout H(lw.hand, B);
+  return rot ? ipm_s<true>(S, P, B, x0, ul, xr, hs, uo, xo, st, its, H.list, H.c_list, lw.ipm, oo, s, nullptr,
                            nullptr, 0)
-             : ipm_s<false>(S, P, B, x0, ul, xr, hs, uo, xo, st, its, lw.hand + 2, lw.hand, lw.ipm, oo, s, nullptr,
+             : ipm_s<false>(S, P, B, x0, ul, xr, hs, uo, xo, st, its, H.list, H.c_list, lw.ipm, oo, s, nullptr,
                             nullptr, 0);
 }
 
 // Re-check of the wave kernel's gap-row QPs that are not SOLVED (status 2, -2, -3, -10): list them,
 // then run the interior point over the list in fp64; a polished point (KKT-checked) becomes SOLVED,
 // a Farkas certificate PRIMAL_INFEASIBLE, anything else keeps the wave kernel's answer. At most
-// kRecheckCap list items are re-checked (one wave per CU at S = 4, N = 20). Count hand[1], list
-// hand + 2; zeroed: the caller's one memset already cleared hand[1].
+// kRecheckCap list items are re-checked (one wave per CU at S = 4, N = 20). Count HandLayout::c_rc,
+// list HandLayout::list (or `flagged`); zeroed: the caller already cleared the count.
 constexpr int kRecheckCap = 4096;
 hipError_t launch_gap_recheck(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                               const float* hs, float* uo, float* xo, int* st, int* its, const LaneWork& lw,
@@ -72,18 +73,19 @@ hipError_t launch_gap_recheck(const KParams& P, int B, const float* x0, const fl
   const int S = lane_ipm_segments(P, cap, l2);
   if (S == 0) return hipSuccess;  // no segmentation fits this horizon: the wave kernel's answer stands
   hipError_t e = hipSuccess;
-  const int* list = flagged ? flagged : lw.hand + 2;
+  const HandLayout H(lw.hand, B);
+  const int* list = flagged ? flagged : H.list;
   if (!flagged) {
-    if (!zeroed && (e = hipMemsetAsync(lw.hand + 1, 0, sizeof(int), s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(ipm_flag_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, st, lw.hand + 1, lw.hand + 2);
+    if (!zeroed && (e = hipMemsetAsync(H.c_rc, 0, sizeof(int), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(ipm_flag_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, st, H.c_rc, H.list);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   const bool rot = lw.rot && P.q[0] == P.q[1];
   // grid of `cap` QPs; the kernel reads the count and idle waves exit at once
   return rot ? ipm_s<true>(S, P, cap, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, lw.ipm, oo, s,
-                           list, lw.hand + 1, 1)
+                           list, H.c_rc, 1)
              : ipm_s<false>(S, P, cap, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, lw.ipm, oo, s,
-                            list, lw.hand + 1, 1);
+                            list, H.c_rc, 1);
 }
 
 }  // namespace f110qp

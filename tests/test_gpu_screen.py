@@ -80,3 +80,23 @@ def test_screen_infeasible_and_non_finite(oracle, capi, monkeypatch):
     # non-finite state: NUMERICAL; a non-finite gap row: the wave kernel's empty-set verdict
     assert st[5] == capi.NUMERICAL and st[9] == capi.PRIMAL_INFEASIBLE
     np.testing.assert_array_equal(st, out["wave"][2])
+
+
+def test_early_gi_matches_screen_without_it(oracle, capi, monkeypatch):
+    """The early GI (predicted-heaviest QPs on the aux stream, concurrently with the box solve)
+    changes only when GI starts: the same statuses and optimum as the screen without it
+    (F110QP_GAP_EARLY=0), both against the oracle; a small K forces both GI launches to share
+    the batch and the re-check list."""
+    N, B = 20, 2048
+    w, hs = _gap_batch(oracle, B, N, 333, lateral=0.8)
+    out = {}
+    for name, k in (("off", "0"), ("k16", "16"), ("default", None)):
+        if k is None:
+            monkeypatch.delenv("F110QP_GAP_EARLY", raising=False)
+        else:
+            monkeypatch.setenv("F110QP_GAP_EARLY", k)
+        out[name] = check(oracle, capi, N, w, hs, gap=True)
+    for name in ("k16", "default"):
+        np.testing.assert_array_equal(out[name][2], out["off"][2])
+        ok = out["off"][2] == capi.SOLVED
+        assert rel_err(out[name][0][ok], out["off"][0][ok].astype(np.float64)).max() <= 1e-6
