@@ -107,7 +107,8 @@ struct f110qp_ctx {
   int lane_seg = 0;          // lane horizon segments per QP (LaneWork::seg: 0 auto, 1 off, 2/4/8)
   int lane_seg32 = 0;        // segmented kernel: force fp32 references + scratch (LaneWork::seg32)
   int gap_screen = -1;      // gap rows, AUTO: box screen on the lane kernel (-1 by batch, 0 off, 1 on)
-  int gap_early = 256;      // screen: predicted-heaviest QPs whose GI starts with the box solve
+  int gap_early = 0;        // screen: predicted-heaviest QPs whose GI starts with the box solve
+                            // (F110QP_GAP_EARLY; off: same-box C3 207 us without, 231-235 with 256)
   hipStream_t aux = nullptr;             // second stream of the screen path (highest priority)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipStream_t stream = nullptr;
@@ -230,6 +231,7 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
   // test hook: F110QP_LANE_SEG_F32=1 forces the segmented kernel's float references and scratch
   if (const char* ef = std::getenv("F110QP_LANE_SEG_F32")) c->lane_seg32 = std::atoi(ef) != 0;
   if (const char* eg = std::getenv("F110QP_GAP_SCREEN")) c->gap_screen = std::atoi(eg) != 0;
+  if (const char* eg = std::getenv("F110QP_GI_GAPFIRST")) c->kp.gap_first = std::atoi(eg) != 0;
   if (const char* ee = std::getenv("F110QP_GAP_EARLY")) {  // 0: no early GI
     const int v = std::atoi(ee);
     if (v >= 0 && v <= (1 << 20)) c->gap_early = v;

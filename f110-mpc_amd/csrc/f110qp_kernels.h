@@ -25,6 +25,7 @@ struct KParams {
   int xr_stride;  // points per QP in x_ref (>= N; the reference passes its whole miniPath)
   int pdas_max;   // PDAS passes of the wave kernel's box path before its GI loop takes over
   int pass_cap = 0;  // lane kernels: passes per launch (0: max_iter; measurement knob F110QP_LANE_PASSCAP)
+  int gap_first = 1;  // wave GI with gap rows: a violated gap row is added before any box row
 };
 
 // Warm-start state of a context (all null = cold solve). Per QP slot b of the batch:

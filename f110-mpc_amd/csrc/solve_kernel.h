@@ -1446,9 +1446,13 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     } else {
       float X[R], Y[R];
       if (GAP) rollout_lin_f32<R>(sm.M, lane, xv, X, Y);
-      float best = 0.f;
-      int bid = 0x7fffffff;
-      float sraw = 0.f;  // raw slack of this lane's best candidate
+      // Gap rows first (P.gap_first): a violated gap row enters before any box row; numpy model of
+      // the GI loop on the C3 batch (tests/diag_gi_selection_model.py rules): max 34 -> 30
+      // iterations, p99 17 either way. Otherwise one ranking over all rows.
+      const bool gf = GAP && P.gap_first;
+      float best = 0.f, bestG = 0.f;
+      int bid = 0x7fffffff, bidG = 0x7fffffff;
+      float sraw = 0.f, srawG = 0.f;  // raw slack of this lane's best candidate (box / gap class)
 #pragma unroll
       for (int r = 0; r < R; r++) {
         if (!valid[r]) continue;
@@ -1460,15 +1464,31 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         if (GAP) {
           const float s2 = (a ? ga1 : ga0) * X[r] + (a ? gb1 : gb0) * Y[r] + cgap[r];
           const float v2 = s2 * gsc[r];  // ranked by the W-norm (steepest edge), thresholded as before
-          if (!(actf[r] & 4) && s2 < -1e-6f * gnorm && v2 < best) { best = v2; bid = 3 * v + 2; sraw = s2; }
+          const bool c2 = !(actf[r] & 4) && s2 < -1e-6f * gnorm;
+          if (gf) {
+            if (c2 && v2 < bestG) { bestG = v2; bidG = 3 * v + 2; srawG = s2; }
+          } else if (c2 && v2 < best) {
+            best = v2; bid = 3 * v + 2; sraw = s2;
+          }
         }
       }
-      int bid_w = bid;
-      float best_w = best;
-      wave_argmin(best_w, bid_w);
+      int bid_w = 0x7fffffff;
+      float sraw_w = sraw;
+      if (gf) {
+        float bg = bestG;
+        bid_w = bidG;
+        wave_argmin(bg, bid_w);
+        sraw_w = srawG;
+      }
+      if (bid_w == 0x7fffffff) {
+        float best_w = best;
+        bid_w = bid;
+        wave_argmin(best_w, bid_w);
+        sraw_w = sraw;
+      }
       if (bid_w != 0x7fffffff) {
         p = bid_w;
-        sp = readlane_f(sraw, (bid_w / 3) & 63);
+        sp = readlane_f(sraw_w, (bid_w / 3) & 63);
       } else {
         // ---- 5. refinement in fp64 + exact feasibility re-check ----
         STAMP(t_ref0);
