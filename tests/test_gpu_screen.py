@@ -100,3 +100,44 @@ def test_early_gi_matches_screen_without_it(oracle, capi, monkeypatch):
         np.testing.assert_array_equal(out[name][2], out["off"][2])
         ok = out["off"][2] == capi.SOLVED
         assert rel_err(out[name][0][ok], out["off"][0][ok].astype(np.float64)).max() <= 1e-6
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_screen_fuzz_configs_against_oracle(oracle, capi, seed):
+    """The AUTO gap path at screen sizes (1,024..1,600 QPs) over random corners of the ABI's
+    parameter space (horizon, dt, weights incl. zero state weights, u_des on a bound, narrow
+    bounds): exact status parity with the oracle (QPs it cannot certify excluded, as in
+    test_gpu_parity.test_fuzz_configs_against_oracle), the optimum and objective to tolerance."""
+    rng = np.random.default_rng(7100 + seed)
+    for case in range(2):
+        N = int(rng.choice([5, 13, 20, 27, 33, 40, 48]))
+        lo0, lo1 = float(rng.uniform(1.0, 3.5)), float(rng.uniform(-0.6, -0.1))
+        hi0, hi1 = lo0 + float(rng.uniform(0.3, 2.0)), -lo1 * float(rng.uniform(0.5, 1.5))
+        ud = [float(rng.choice([hi0, lo0, 0.5 * (lo0 + hi0)])), float(rng.choice([0.0, hi1, lo1]))]
+        q01 = float(rng.choice([0.0, 1.0, 10.0, 40.0]))
+        over = dict(q=[q01, q01 if rng.random() < 0.5 else float(rng.uniform(0.5, 20.0)),
+                       float(rng.choice([0.0, 0.5, 3.0]))],
+                    r=[float(rng.uniform(0.05, 2.0)), float(rng.uniform(0.5, 10.0))], u_des=ud,
+                    u_min=[lo0, lo1], u_max=[hi0, hi1])
+        dt = float(np.float32(rng.choice([0.005, 0.01, 0.02, 0.05])))
+        B = int(rng.integers(1024, 1600))
+        w = workload.make_batch(B, N, seed=int(rng.integers(1 << 30)), heading="true",
+                                lateral=float(rng.uniform(0.0, 1.5)), steer_range=float(rng.uniform(0.0, 0.8)))
+        ranges, amin, ainc, amax = workload.make_scans(B, seed=int(rng.integers(1 << 30)))
+        hs = halfspaces_oracle(oracle, w["x0"], ranges, (amin, ainc, amax))
+        s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE, dt=dt, **over))
+        assert s.gap_screen(B)
+        u, x, st, it, ob, co = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs, objective=True)
+        s.close()
+        prm = oracle.params(N, dt=dt, **over)
+        ur, xr, sr, obr = oracle.solve_batch(prm, w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=True,
+                                             objective=True)
+        tag = (seed, case, N, dt, B, over)
+        cmp = sr != oracle.UNCERTIFIED
+        assert (sr == oracle.UNCERTIFIED).sum() <= max(1, 0.02 * B), tag
+        np.testing.assert_array_equal(st[cmp], sr[cmp], err_msg=str(tag))
+        ok = sr == oracle.SOLVED
+        if ok.any():
+            assert rel_err(u[ok], ur[ok]).max() <= 1e-4, tag
+            assert rel_err(x[ok], xr[ok]).max() <= 1e-4, tag
+            np.testing.assert_allclose(ob[ok], obr[ok], rtol=1e-6, atol=1e-6, err_msg=str(tag))
