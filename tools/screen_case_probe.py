@@ -58,6 +58,7 @@ def main():
         ewb = rel_err(res["wave_box"][0], ubr)
         bad = np.where(ok & (ea > 1e-4))[0]
         out = dict(N=N, dt=dt, B=B, over=over, lane_info=res["lane_info"], n_bad=int(len(bad)),
+                   n_status_mismatch=int(((res["auto"][2] != sr) & (sr != oracle.UNCERTIFIED)).sum()),
                    max_err_auto=float(ea[ok].max()), max_err_wave=float(ew[ok].max()),
                    max_err_lane_box=float(elb[sbr == 1].max()), max_err_wave_box=float(ewb[sbr == 1].max()),
                    n_lane_box_bad=int((elb[sbr == 1] > 1e-4).sum()),
