@@ -305,6 +305,42 @@ def _halfspaces_host(w, B):
     return hs
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list, print_only: bool = False) -> int:
+    """`bench.py --gpus N` without a launcher: start N child processes of this script, one per GPU
+    (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1), before this process touches
+    the GPU; the children's output passes through (rank 0 prints the JSON line). Returns the exit
+    code: 0 only if every rank exited 0."""
+    import subprocess
+
+    port = _free_port()
+    envs = []
+    for i in range(n):
+        e = dict(os.environ)
+        e.update(RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    cmd = [sys.executable, os.path.abspath(__file__)] + argv
+    if print_only:
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+        print(json.dumps({"cmd": cmd, "ranks": [{k: e[k] for k in keys} for e in envs]}))
+        return 0
+    procs = [subprocess.Popen(cmd, env=e) for e in envs]
+    codes = [p.wait() for p in procs]
+    bad = [(i, c) for i, c in enumerate(codes) if c != 0]
+    if bad:
+        print(f"bench.py: ranks failed (rank, exit code): {bad}", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -332,7 +368,22 @@ def main():
     ap.add_argument("--backend", default="auto", choices=["auto", "wave", "lane"],
                     help="solver back end (auto: lane-per-QP for box-only batches >= capi.LANE_MIN_BATCH = 1024 "
                          "at N <= 32, >= capi.LANE_MIN_BATCH_WIDE = 1 at N > 32; f110qp_backend_info)")
+    ap.add_argument("--print-launch", action="store_true", help=argparse.SUPPRESS)  # test hook: the rank plan
     args = ap.parse_args()
+
+    # one process per GPU: under torch.distributed.run (WORLD_SIZE set) it must agree with --gpus;
+    # without a launcher, --gpus N > 1 starts the N ranks itself (before any GPU call here)
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}: refusing to run "
+                  f"a different number of ranks than asked for", file=sys.stderr)
+            sys.exit(2)
+    elif args.gpus > 1:
+        argv = [a for a in sys.argv[1:] if a != "--print-launch"]
+        sys.exit(launch_ranks(args.gpus, argv, print_only=args.print_launch))
+    elif args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
@@ -572,8 +623,8 @@ def main():
     achieved_gbs = bpq * Bper / (kms * 1e-3) / 1e9
     achieved_tf = fpq * Bper / (kms * 1e-3) / 1e12
     # the PMC summary's back-end key (tools/summarize_profiles.py KERNELS): the partitioned-horizon
-    # kernel is "lane_seg", the interior point (gap rows on the lane back end) "lane_ipm"
-    prof_be = be_name if be_name == "wave" else ("lane_ipm" if gap else ("lane_seg" if lane_seg > 1 else "lane"))
+    # kernel is "lane_seg"
+    prof_be = be_name if be_name == "wave" else ("lane_seg" if lane_seg > 1 else "lane")
     traffic = load_traffic(args.config, Bper, N, prof_be)
 
     out = {
@@ -597,8 +648,8 @@ def main():
             "gap_rows": bool(gap),
             "warm_start": bool(warm),
             "backend": {"wave": "wave-per-QP (condensed, PDAS/GI)",
-                        "lane": "lane-per-QP (Riccati interior point fp64 + GI hand-over)" if gap else
-                                "lane-per-QP (Riccati/PDAS fp64)"}[be_name]
+                        "lane": "lane-per-QP box screen (Riccati/PDAS fp64) + wave GI for the QPs it does not "
+                                "clear" if gap else "lane-per-QP (Riccati/PDAS fp64)"}[be_name]
                        + (" grouped: one W = H^-1 per scenario" if grouped and be_name == "wave" else ""),
             **({"lane_qps_per_wave": lane_qpw, "lane_scratch": capi.SCRATCH_NAMES[lane_scr],
                 "lane_segments": lane_seg}
@@ -629,11 +680,10 @@ def main():
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
             "kernel": {"wave": "f110qp::solve_kernel",
-                       "lane": (f"f110qp::lane_ipm_kernel<{lane_seg}> (interior point) + the wave kernel over its "
-                                "hand-over list" if gap else
-                                ("f110qp::lane_kernel" if lane_seg == 1 else
-                                 f"f110qp::lane_seg_kernel<{lane_seg}> (partitioned horizon)")
-                                + " (the only launch of the step)")}[be_name],
+                       "lane": ("f110qp::lane_kernel" if lane_seg == 1 else
+                                f"f110qp::lane_seg_kernel<{lane_seg}> (partitioned horizon)")
+                               + (" box screen + the wave kernel's GI over its list" if gap else
+                                  " (the only launch of the step)")}[be_name],
             "kernel_ms_per_launch": kms,
             "algorithmic_bytes_per_qp": bpq,
             cname: {"achieved": achieved_tf, "peak": cpeak, "unit": "TFLOP/s",

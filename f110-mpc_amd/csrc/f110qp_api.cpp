@@ -97,8 +97,7 @@ struct f110qp_ctx {
   DevBuf gW, gkey, glead;    // grouped mode: W = H^-1, key and leader per group
   DevBuf dgrp;               // host-pointer grouped calls: device copy of the group ids
   DevBuf lscr;               // lane back end: HBM Riccati scratch (when not in LDS)
-  DevBuf hand;               // gap rows: two counts, one list, the screen priorities (2B + 2 ints)
-  f110qp::IpmKnobs ipm;      // lane back end, gap rows: interior-point knobs (test/bench hooks)
+  DevBuf hand;               // gap rows: counts and lists (f110qp::HandLayout, kHandInts(B) ints)
   int lane_kmax = 16;        // lane back end: PDAS passes before single (least-index) flips
   int lane_mode = 0;         // lane scratch placement (LaneWork::mode)
   int lane_qpw = 0;          // lane QPs per wave (LaneWork::qpw, 0 = auto)
@@ -107,10 +106,6 @@ struct f110qp_ctx {
   int lane_seg = 0;          // lane horizon segments per QP (LaneWork::seg: 0 auto, 1 off, 2/4/8)
   int lane_seg32 = 0;        // segmented kernel: force fp32 references + scratch (LaneWork::seg32)
   int gap_screen = -1;      // gap rows, AUTO: box screen on the lane kernel (-1 by batch, 0 off, 1 on)
-  int gap_early = 0;        // screen: predicted-heaviest QPs whose GI starts with the box solve
-                            // (F110QP_GAP_EARLY; off: same-box C3 207 us without, 231-235 with 256)
-  hipStream_t aux = nullptr;             // second stream of the screen path (highest priority)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipStream_t stream = nullptr;
 };
 
@@ -204,38 +199,10 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     const int v = std::atoi(es);
     if (v == 0 || v == 1 || v == 2 || v == 4 || v == 8) c->lane_seg = v;
   }
-  c->ipm.tolp = c->ipm.told = 1e-8;
-  // test/bench hooks of the interior-point lane kernel (gap rows): polish threshold on mu,
-  // acceptance tolerance, iteration cap before the hand-over to the wave kernel
-  if (const char* ev = std::getenv("F110QP_IPM_POLMU")) {
-    const double v = std::atof(ev);
-    if (v > 0.0) c->ipm.pol_mu = v;
-  }
-  if (const char* ev = std::getenv("F110QP_IPM_TOL")) {
-    const double v = std::atof(ev);
-    if (v > 0.0 && v < 1e-3) c->ipm.tolp = c->ipm.told = v;
-  }
-  if (const char* ev = std::getenv("F110QP_IPM_MAXIT")) {
-    const int v = std::atoi(ev);
-    if (v >= 0 && v <= 200) c->ipm.max_iter = v;
-  }
-  if (const char* ev = std::getenv("F110QP_IPM_DEBUG")) c->ipm.debug = std::atoi(ev);
-  if (const char* ev = std::getenv("F110QP_IPM_ACTSIG")) {
-    const double v = std::atof(ev);
-    if (v > 0.0) c->ipm.act_sig = v;
-  }
-  if (const char* ev = std::getenv("F110QP_IPM_SFLOOR")) {
-    const double v = std::atof(ev);
-    if (v > 0.0) c->ipm.s_floor = v;
-  }
   // test hook: F110QP_LANE_SEG_F32=1 forces the segmented kernel's float references and scratch
   if (const char* ef = std::getenv("F110QP_LANE_SEG_F32")) c->lane_seg32 = std::atoi(ef) != 0;
   if (const char* eg = std::getenv("F110QP_GAP_SCREEN")) c->gap_screen = std::atoi(eg) != 0;
   if (const char* eg = std::getenv("F110QP_GI_GAPFIRST")) c->kp.gap_first = std::atoi(eg) != 0;
-  if (const char* ee = std::getenv("F110QP_GAP_EARLY")) {  // 0: no early GI
-    const int v = std::atoi(ee);
-    if (v >= 0 && v <= (1 << 20)) c->gap_early = v;
-  }
   if (const char* ep = std::getenv("F110QP_LANE_PASSCAP")) {  // measurement: passes per lane launch
     const int v = std::atoi(ep);
     if (v > 0 && v < 1000) c->kp.pass_cap = v;
@@ -261,9 +228,6 @@ void f110qp_destroy(f110qp_ctx* c) {
   c->hand.release();
   c->gW.release(); c->gkey.release(); c->glead.release(); c->dgrp.release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  if (c->aux) (void)hipStreamDestroy(c->aux);
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   delete c;
 }
 
@@ -304,17 +268,14 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
 }
 
 // The back end a call of `batch` QPs runs on (what AUTO resolves to). Box rows: the lane back end
-// from F110QP_LANE_MIN_BATCH[_WIDE]. Gap rows: AUTO keeps the wave kernel (its GI measured 290 us
-// on C3 against 1,010 us for the lane interior point); an explicit
-// F110QP_BACKEND_LANE runs the interior point wherever its LDS fits (lane_ipm_segments > 0), else
-// the wave kernel.
-static int resolve_backend(f110qp_ctx* c, int batch, bool grouped, const f110qp::LaneWork& lw) {
+// from F110QP_LANE_MIN_BATCH[_WIDE]. Gap rows: the wave kernel's GI (AUTO, WAVE), behind the box
+// screen on the lane kernel for AUTO batches >= F110QP_GAP_SCREEN_MIN_BATCH; LANE: the box screen
+// on the lane kernel for every batch (GI for the QPs it does not clear).
+static int resolve_backend(f110qp_ctx* c, int batch, bool grouped) {
   const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
   int be = c->cfg.backend;
-  if (gap) {
-    if (be != F110QP_BACKEND_LANE) return F110QP_BACKEND_WAVE;
-    return f110qp::lane_ipm_segments(c->kp, batch, lw) > 0 ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
-  }
+  if (gap)  // LANE: the screen path (never grouped or warm-started: those run GI on the wave kernel)
+    return be == F110QP_BACKEND_LANE && !grouped && !c->cfg.warm_start ? F110QP_BACKEND_LANE : F110QP_BACKEND_WAVE;
   if (be == F110QP_BACKEND_AUTO) {
     const int min_b = grouped ? (c->cfg.horizon <= 32 ? F110QP_LANE_MIN_BATCH_GROUPED
                                                       : F110QP_LANE_MIN_BATCH_GROUPED_WIDE)
@@ -325,12 +286,12 @@ static int resolve_backend(f110qp_ctx* c, int batch, bool grouped, const f110qp:
   return be;
 }
 
-// Gap rows on the wave back end: does the call take the box screen on the lane kernel first
-// (F110QP_GAP_SCREEN_MIN_BATCH; AUTO only, ungrouped, no warm-start state)?
+// Gap rows: does the call take the box screen on the lane kernel first (backend LANE, or AUTO from
+// F110QP_GAP_SCREEN_MIN_BATCH; ungrouped, no warm-start state)?
 static bool gap_screen(const f110qp_ctx* c, int batch, bool grouped) {
-  if (c->cfg.gap_mode != F110QP_GAP_ACTIVE || c->cfg.backend != F110QP_BACKEND_AUTO || grouped ||
-      c->cfg.warm_start || c->gap_screen == 0)
-    return false;
+  if (c->cfg.gap_mode != F110QP_GAP_ACTIVE || grouped || c->cfg.warm_start) return false;
+  if (c->cfg.backend == F110QP_BACKEND_LANE) return true;
+  if (c->cfg.backend != F110QP_BACKEND_AUTO || c->gap_screen == 0) return false;
   return c->gap_screen == 1 || batch >= F110QP_GAP_SCREEN_MIN_BATCH;
 }
 
@@ -345,35 +306,17 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   lw->dref = c->lane_dref;
   lw->seg = c->lane_seg;
   lw->seg32 = c->lane_seg32;
-  lw->ipm = c->ipm;
-  *backend = resolve_backend(c, batch, grouped, *lw) == F110QP_BACKEND_LANE ? f110qp::BACKEND_LANE
-                                                                           : f110qp::BACKEND_WAVE;
+  *backend = resolve_backend(c, batch, grouped) == F110QP_BACKEND_LANE ? f110qp::BACKEND_LANE
+                                                                      : f110qp::BACKEND_WAVE;
   (void)s;
   hipError_t e;
   if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) {
-    // count + list of the interior point's hand-over (lane back end) or of the fp64 re-check of
-    // the wave kernel's non-SOLVED QPs (wave back end)
-    if ((e = c->hand.ensure((5 * (size_t)batch + 4) * sizeof(int))) != hipSuccess)  // f110qp::HandLayout
-      return hip_fail(e, "hipMalloc hand-over list");
+    // counts and lists of the screen's GI list and of the fp64 re-check
+    if ((e = c->hand.ensure(f110qp::kHandInts(batch) * sizeof(int))) != hipSuccess)
+      return hip_fail(e, "hipMalloc gap-row lists");
     lw->hand = (int*)c->hand.p;
-    lw->screen = *backend == f110qp::BACKEND_WAVE && gap_screen(c, batch, grouped);
+    lw->screen = gap_screen(c, batch, grouped);
     if (!lw->screen) return F110QP_OK;
-    if (c->gap_early > 0) {  // the early GI's stream and events (created once, on the current device)
-      if (!c->aux) {
-        int lo = 0, hi = 0;
-        if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess ||
-            (e = hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, hi)) != hipSuccess)
-          return hip_fail(e, "hipStreamCreate (screen aux stream)");
-      }
-      if (!c->ev_fork && (e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess)
-        return hip_fail(e, "hipEventCreate");
-      if (!c->ev_join && (e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess)
-        return hip_fail(e, "hipEventCreate");
-      lw->early = c->gap_early;
-      lw->aux = c->aux;
-      lw->ev_fork = c->ev_fork;
-      lw->ev_join = c->ev_join;
-    }
   } else if (*backend == f110qp::BACKEND_WAVE) {
     return F110QP_OK;
   }
@@ -509,20 +452,19 @@ int f110qp_backend_info(f110qp_ctx* c, int batch, int grouped, int* backend, int
                         int* scratch) {
   if (!c) return fail(F110QP_ERR_INVALID, "ctx is NULL");
   if (batch < 1) return fail(F110QP_ERR_INVALID, "batch must be >= 1");
-  const bool gap = c->cfg.gap_mode == F110QP_GAP_ACTIVE;
   f110qp::LaneWork lw;
   lw.mode = c->lane_mode;
   lw.qpw = c->lane_qpw;
   lw.seg = c->lane_seg;
-  const int be = resolve_backend(c, batch, grouped != 0, lw);
-  const bool lane = be == F110QP_BACKEND_LANE;
-  const int segs = lane ? (gap ? f110qp::lane_ipm_segments(c->kp, batch, lw) : f110qp::lane_segments(c->kp, batch, lw)) : 1;
+  const int be = resolve_backend(c, batch, grouped != 0);
+  const bool lane = be == F110QP_BACKEND_LANE;  // gap rows: the box screen's lane solve
+  const int segs = lane ? f110qp::lane_segments(c->kp, batch, lw) : 1;
   if (backend) *backend = be;
   if (qps_per_wave) *qps_per_wave = lane ? (segs > 1 ? 64 / segs : f110qp::lane_qps_per_wave(batch, lw.qpw)) : 1;
   lw.seg32 = c->lane_seg32;
   if (scratch)
-    *scratch = !lane ? 0 : gap ? 1 : segs > 1 ? f110qp::lane_seg_scratch(c->kp, batch, segs, lw)
-                                              : f110qp::lane_scratch_mode(c->kp, batch, lw);
+    *scratch = !lane ? 0 : segs > 1 ? f110qp::lane_seg_scratch(c->kp, batch, segs, lw)
+                                    : f110qp::lane_scratch_mode(c->kp, batch, lw);
   return F110QP_OK;
 }
 
@@ -537,7 +479,6 @@ int f110qp_lane_segments(f110qp_ctx* c, int batch, int* segments) {
   lw.qpw = c->lane_qpw;
   lw.seg = c->lane_seg;
   if (be != F110QP_BACKEND_LANE) *segments = 1;
-  else if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) *segments = f110qp::lane_ipm_segments(c->kp, batch, lw);
   else *segments = f110qp::lane_segments(c->kp, batch, lw);
   return F110QP_OK;
 }
@@ -545,9 +486,7 @@ int f110qp_lane_segments(f110qp_ctx* c, int batch, int* segments) {
 int f110qp_gap_screen(f110qp_ctx* c, int batch, int* on) {
   if (!c || !on) return fail(F110QP_ERR_INVALID, "ctx / on is NULL");
   if (batch < 1) return fail(F110QP_ERR_INVALID, "batch must be >= 1");
-  f110qp::LaneWork lw;
-  lw.seg = c->lane_seg;
-  *on = resolve_backend(c, batch, false, lw) == F110QP_BACKEND_WAVE && gap_screen(c, batch, false);
+  *on = gap_screen(c, batch, false);
   return F110QP_OK;
 }
 

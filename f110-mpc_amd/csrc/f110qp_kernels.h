@@ -47,32 +47,18 @@ struct WarmState {
   int ngroups = 0;
 };
 
-// Knobs of the interior-point lane kernel for QPs with gap rows (lane_ipm_kernel.h).
-struct IpmKnobs {
-  double pol_mu = 1e-3;  // polish once a QP's mu (mean complementarity) is below this
-  double tolp = 1e-9;    // polish acceptance: row violation, x (1 + |bound|)
-  double told = 1e-9;    // polish acceptance: multiplier sign of an active row
-  double tau = 0.995;    // fraction to the boundary
-  double act_sig = 1e4;  // polish: a row is guessed active when z > act_sig * s (Sig = z / s >= act_sig)
-  double s_floor = 1.0;  // initial slack floor
-  int max_iter = 30;     // interior-point iterations before the hand-over to the wave kernel
-  int debug = 0;         // test hook: return every QP's current iterate as SOLVED (no polish test)
-};
-
-// LaneWork::hand for a call of B gap-row QPs: four counts, then five B-int arrays.
+// LaneWork::hand for a call of B gap-row QPs: kHandInts(B) = 3 B + 4 ints, the two counts first
+// (padded to four ints), then three B-int arrays.
 struct HandLayout {
-  int* c_list;   // [0] GI list count (hand-over of the interior point, or the screen's GI list)
-  int* c_rc;     // [1] the fp64 re-check's count
-  int* c_early;  // [2] the early GI list's count
-  int* list;     // GI list (hand-over / screen), and the re-check list of the flag kernel
-  int* prio;     // screen: GI priority per QP
-  int* rc;       // re-check list the GI kernel appends to
-  int* mark;     // early: 1 for the QPs GI takes on the aux stream
-  int* elist;    // early GI list
+  int* c_list;  // [0] the screen's GI list count
+  int* c_rc;    // [1] the fp64 re-check's count (the wave kernel appends its non-SOLVED QPs)
+  int* list;    // [4, 4 + B) the screen's GI list, heavy first
+  int* prio;    // [4 + B, 4 + 2B) screen: GI priority per QP
+  int* rc;      // [4 + 2B, 4 + 3B) the re-check list
   HandLayout(int* h, int B)
-      : c_list(h), c_rc(h + 1), c_early(h + 2), list(h + 4), prio(h + 4 + (size_t)B),
-        rc(h + 4 + 2 * (size_t)B), mark(h + 4 + 3 * (size_t)B), elist(h + 4 + 4 * (size_t)B) {}
+      : c_list(h), c_rc(h + 1), list(h + 4), prio(h + 4 + (size_t)B), rc(h + 4 + 2 * (size_t)B) {}
 };
+constexpr size_t kHandInts(int B) { return 3 * (size_t)B + 4; }
 
 // Workspace of the lane-per-QP kernel (lane_kernel.h): the HBM Riccati scratch when it does
 // not stay in LDS (ceil(B/L) x N x 8 x L doubles at most, L QPs per wave <= 64).
@@ -85,14 +71,9 @@ struct LaneWork {
   int dref = 1;   // 1: fp64 references in LDS when the resident waves fit (DREF); 0: float
   int seg = 0;    // horizon segments per QP (lane_seg_kernel.h): 0 auto, 1 off, 2 / 4 / 8 forced
   int seg32 = 0;  // segmented kernel: 1 forces float references and Riccati scratch in LDS
-  int* hand = nullptr;  // gap rows: counts + per-QP lists, layout HandLayout below (5 B + 4 ints)
-  int screen = 0;       // gap rows, wave back end: box solve on the lane kernel first, GI only
-                        // for the QPs whose box optimum violates a gap row (f110qp_kernels.hip)
-  int early = 0;        // screen: GI for up to this many predicted-heavy QPs on the aux stream,
-                        // concurrently with the box solve (0: off)
-  hipStream_t aux = nullptr;  // the context's second stream and its fork / join events
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  IpmKnobs ipm;
+  int* hand = nullptr;  // gap rows: counts + per-QP lists (HandLayout, kHandInts(B) ints)
+  int screen = 0;       // gap rows: box solve on the lane kernel first, GI only for the QPs whose
+                        // box optimum violates a gap row (f110qp_kernels.hip)
 };
 
 // Optional per-QP objective outputs (fp64, computed in the kernels' output sweeps from the fp64
@@ -107,7 +88,6 @@ struct ObjOut {
   // gap rows it violates; null: no screen)
   const float* scr_hs = nullptr;
   int* scr_prio = nullptr;
-  const int* scr_skip = nullptr;  // QPs the early GI owns: no outputs from the box solve
   // wave kernel, gap rows: QPs it does not report SOLVED are appended here for the fp64 re-check
   // (count + list; null: the re-check flags them itself)
   int* rc_count = nullptr;
@@ -125,32 +105,20 @@ int lane_segments(const KParams& P, int B, const LaneWork& lw);
 // scratch of the segmented kernel at S segments: 1 LDS fp64, 2 LDS fp32 (lane_seg_kernel.h)
 int lane_seg_scratch(const KParams& P, int B, int S, const LaneWork& lw);
 
-// Horizon segments per QP of the interior-point lane kernel for a batch WITH gap rows
-// (lane_ipm_kernel.h), or 0 when its LDS does not fit (the wave kernel then takes the batch).
-int lane_ipm_segments(const KParams& P, int B, const LaneWork& lw);
-
-// The interior-point lane kernel alone: QPs it does not polish are appended to the hand-over
-// list (count lw.hand[0], list lw.hand + 2; the count must be zero on entry).
-hipError_t launch_lane_ipm(const KParams& P, int B, const float* x0, const float* u_lin,
-                           const float* x_ref, const float* hs, float* u_out, float* x_out,
-                           int* status, int* iters, const LaneWork& lw, const ObjOut& oo,
-                           hipStream_t stream);
-
-// fp64 re-check of the wave kernel's gap-row QPs it did not report SOLVED (lane_ipm_inst.hip):
-// the interior point over their list; polished -> SOLVED, Farkas certificate -> PRIMAL_INFEASIBLE,
-// else the wave kernel's answer stands. Needs lw.hand (B + 2 ints; count hand[1], zeroed by the
-// caller when `zeroed`; `flagged`: the wave kernel already appended its non-SOLVED QPs to this
-// list, count hand[1]).
+// fp64 re-check of the gap-row QPs the wave kernel did not report SOLVED (its certificate
+// failed, or GI ended infeasible / at its cap): the fp64 Goldfarb-Idnani of gi64_kernel.h over
+// the device-side list (count, list: HandLayout c_rc / rc), every listed QP, its outputs rewritten.
 hipError_t launch_gap_recheck(const KParams& P, int B, const float* x0, const float* u_lin,
                               const float* x_ref, const float* hs, float* u_out, float* x_out,
-                              int* status, int* iters, const LaneWork& lw, const ObjOut& oo,
-                              hipStream_t stream, bool zeroed = false, const int* flagged = nullptr);
+                              int* status, int* iters, const int* list, const int* count,
+                              const ObjOut& oo, hipStream_t stream);
 
 enum Backend { BACKEND_WAVE = 0, BACKEND_LANE = 1 };
 
 // Solve B QPs. hs == nullptr -> box-only kernels (gap rows inactive). backend LANE: box rows, the
-// lane-per-QP Riccati/PDAS kernel alone (one launch, no hand-over); gap rows, the interior-point
-// lane kernel, then the wave kernel over its hand-over list (QPs it did not polish).
+// lane-per-QP Riccati/PDAS kernel alone (one launch, no hand-over). Gap rows: lw.screen, the box
+// solve on the lane kernel, GI for the QPs whose box optimum violates a gap row; else GI for every
+// QP; then the fp64 re-check of what GI did not certify.
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u_lin,
                         const float* x_ref, const float* hs, float* u_out, float* x_out,
                         int* status, int* iters, const WarmState& warm, int backend,

@@ -35,9 +35,6 @@ static hipError_t launch_g(const KParams& P, int B, const float* x0, const float
   return hipErrorInvalidValue;
 }
 
-// waves of the hand-over launch (a work loop over the list; one per CU)
-constexpr int kHandGrid = 256;
-
 // Gap-row screen after a box-only lane solve: a QP whose box optimum keeps every gap row of stages
 // 1..N strictly satisfied has that point as its optimum with the gap rows (adding constraints that
 // hold at the unique minimiser of a strictly convex QP does not move it), so its lane outputs stand.
@@ -109,131 +106,45 @@ __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int*
   }
 }
 
-// Early GI (screen path): the QPs predicted heaviest for GI start on the aux stream while the
-// box solve runs, so the longest chains no longer wait for it. The predictor, per QP: the stages
-// i = 1..N at which the free motion from x0 at the linearisation speed (x0 + v dt i (cos th0,
-// sin th0)) leaves the gap wedge, summed over both rows (numpy model on the C3 batch: the top
-// 128 by this count hold the 10 heaviest QPs for GI, 23 of the 40 heaviest). One workgroup: LDS
-// histogram, descending scan, the first K into the early list with mark[b] = 1; the re-check
-// count is cleared here, before the fork, for the two GI launches that append to it.
-__global__ __launch_bounds__(1024) void gap_presort_kernel(const int B, const int N, const float dt,
-                                                           const float* __restrict__ x0g,
-                                                           const float* __restrict__ ulg,
-                                                           const float* __restrict__ hsg, const int K,
-                                                           int* __restrict__ mark, int* __restrict__ elist,
-                                                           int* __restrict__ ecount, int* __restrict__ rc_count) {
-  __shared__ int hist[kPrioMax + 1];
-  __shared__ int off[kPrioMax + 1];
-  const int t = threadIdx.x;
-  if (t <= kPrioMax) hist[t] = 0;
-  __syncthreads();
-  auto proxy = [&](int b) {
-    const double X = (double)x0g[3 * b], Y = (double)x0g[3 * b + 1], th = (double)x0g[3 * b + 2];
-    const double step = (double)ulg[2 * b] * (double)dt;
-    const double cx = step * cos(th), cy = step * sin(th);
-    const float* h6 = hsg + 6 * (size_t)b;
-    const double a0 = h6[0], b0 = h6[1], c0 = h6[2], a1 = h6[3], b1 = h6[4], c1 = h6[5];
-    int n = 0;
-    for (int i = 1; i <= N; i++) {
-      const double x = X + cx * i, y = Y + cy * i;
-      n += (a0 * x + b0 * y + c0 < 0.0) + (a1 * x + b1 * y + c1 < 0.0);
-    }
-    return min(n, kPrioMax);
-  };
-  for (int b = t; b < B; b += 1024) {
-    const int p = proxy(b);
-    mark[b] = 0;
-    if (p > 0) atomicAdd(&hist[p], 1);
-  }
-  __syncthreads();
-  if (t == 0) {
-    int run = 0;
-    for (int p = kPrioMax; p >= 1; p--) {
-      off[p] = run;
-      run += hist[p];
-    }
-    *ecount = min(run, K);
-    *rc_count = 0;
-  }
-  __syncthreads();
-  for (int b = t; b < B; b += 1024) {
-    const int p = proxy(b);
-    if (p > 0) {
-      const int pos = atomicAdd(&off[p], 1);
-      if (pos < K) {
-        elist[pos] = b;
-        mark[b] = 1;
-      }
-    }
-  }
-}
-
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
                         const float* xr, const float* hs, float* uo, float* xo, int* st,
                         int* its, const WarmState& ws, int backend, const LaneWork& lw,
                         const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (hs && backend == BACKEND_LANE) {
-    // interior point on the lane back end, then the wave kernel's GI over the QPs it handed over
-    // (none in the common case: every wave of that launch reads the zero count and exits)
-    const HandLayout H(lw.hand, B);
-    hipError_t e = hipMemsetAsync(H.c_list, 0, sizeof(int), s);
-    if (e != hipSuccess) return e;
-    if ((e = launch_lane_ipm(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s)) != hipSuccess) return e;
-    return launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), H.list,
-                          H.c_list, B < kHandGrid ? B : kHandGrid, oo, s);
-  }
-  if (hs && lw.screen) {
-    // The box-only lane solve of every QP (the segmented kernel evaluates the screen in its output
-    // sweep, in fp64, and writes each QP's GI priority; the sequential kernel leaves it to
-    // gap_screen_kernel), the GI list heavy first (gap_order_kernel), GI over it (grid B: the waves
-    // past the device-side count exit at once), the fp64 re-check of what GI did not solve (the GI
-    // kernel appends those itself). With the segmented kernel and lw.early, the predicted-heaviest
-    // QPs go to GI first, on the aux stream, concurrently with the box solve, which skips them.
+  if (hs) {
+    // Gap rows. With the screen: the box-only lane solve of every QP (the segmented kernel
+    // evaluates the screen in its output sweep, in fp64, and writes each QP's GI priority; the
+    // sequential kernel leaves it to gap_screen_kernel), the GI list heavy first (gap_order_kernel,
+    // which also zeroes the re-check count), GI over it (grid B: the waves past the device-side
+    // count exit at once). Without: GI for every QP. Either way the GI kernel appends the QPs it
+    // does not certify (SOLVED) to the re-check list, and the fp64 GI re-checks them.
     const HandLayout H(lw.hand, B);
     hipError_t e = hipSuccess;
-    const bool fused = lane_segments(P, B, lw) > 1;
-    const bool early = fused && lw.early > 0 && lw.aux && lw.ev_fork && lw.ev_join;
-    ObjOut go = oo;  // GI: non-SOLVED QPs appended for the re-check
+    ObjOut go = oo;
     go.rc_count = H.c_rc;
     go.rc_list = H.rc;
-    if (early) {
-      const int K = lw.early < B ? lw.early : B;
-      hipLaunchKernelGGL(gap_presort_kernel, dim3(1), dim3(1024), 0, s, B, P.N, P.dt, x0, ul, hs, K, H.mark,
-                         H.elist, H.c_early, H.c_rc);
+    if (lw.screen) {
+      const bool fused = lane_segments(P, B, lw) > 1;
+      ObjOut so = oo;
+      if (fused) {
+        so.scr_hs = hs;
+        so.scr_prio = H.prio;
+      }
+      if ((e = launch_lane(P, B, x0, ul, xr, uo, xo, st, its, WarmState(), lw, so, s)) != hipSuccess) return e;
+      if (!fused) {
+        hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st, H.prio);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL(gap_order_kernel, dim3(1), dim3(1024), 0, s, B, H.prio, H.c_list, H.list, H.c_rc);
       if ((e = hipGetLastError()) != hipSuccess) return e;
-      if ((e = hipEventRecord(lw.ev_fork, s)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(lw.aux, lw.ev_fork, 0)) != hipSuccess) return e;
-      e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), H.elist, H.c_early,
-                         K, go, lw.aux);
-      if (e != hipSuccess) return e;
-      if ((e = hipEventRecord(lw.ev_join, lw.aux)) != hipSuccess) return e;
+      e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), H.list, H.c_list, B,
+                         go, s);
+    } else {
+      if ((e = hipMemsetAsync(H.c_rc, 0, sizeof(int), s)) != hipSuccess) return e;
+      e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr, nullptr, B, go, s);
     }
-    ObjOut so = oo;
-    if (fused) {
-      so.scr_hs = hs;
-      so.scr_prio = H.prio;
-      so.scr_skip = early ? H.mark : nullptr;
-    }
-    if ((e = launch_lane(P, B, x0, ul, xr, uo, xo, st, its, WarmState(), lw, so, s)) != hipSuccess) return e;
-    if (!fused) {
-      hipLaunchKernelGGL(gap_screen_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, P.N, x0, hs, xo, st, H.prio);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(gap_order_kernel, dim3(1), dim3(1024), 0, s, B, H.prio, H.c_list, H.list,
-                       early ? nullptr : H.c_rc);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, WarmState(), H.list, H.c_list, B,
-                       go, s);
     if (e != hipSuccess) return e;
-    if (early && (e = hipStreamWaitEvent(s, lw.ev_join, 0)) != hipSuccess) return e;
-    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s, true, H.rc);
-  }
-  if (hs) {
-    hipError_t e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
-                                  nullptr, B, oo, s);
-    if (e != hipSuccess) return e;
-    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s);
+    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, H.rc, H.c_rc, oo, s);
   }
   if (backend == BACKEND_LANE) return launch_lane(P, B, x0, ul, xr, uo, xo, st, its, ws, lw, oo, s);
   return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, ws, nullptr,
@@ -268,7 +179,7 @@ hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const 
                                 int* its, const WarmState& gws, int* leader, int backend,
                                 const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (backend == BACKEND_LANE)  // per-QP Riccati / interior point: nothing to share
+  if (backend == BACKEND_LANE || (hs && lw.screen))  // per-QP Riccati: nothing to share
     return launch_solve(P, B, x0, ul, xr, hs, uo, xo, st, its, WarmState(), backend, lw, oo, s);
   hipError_t e = hipMemsetAsync(leader, 0x7f, (size_t)gws.ngroups * sizeof(int), s);
   if (e != hipSuccess) return e;
@@ -279,9 +190,14 @@ hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const 
          : launch_prep_g<false>(P, B, x0, ul, xr, hs, gws, leader, s);
   if (e != hipSuccess) return e;
   if (hs) {
-    e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, gws, nullptr, nullptr, B, oo, s);
+    const HandLayout H(lw.hand, B);
+    ObjOut go = oo;
+    go.rc_count = H.c_rc;
+    go.rc_list = H.rc;
+    if ((e = hipMemsetAsync(H.c_rc, 0, sizeof(int), s)) != hipSuccess) return e;
+    e = launch_g<true>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, gws, nullptr, nullptr, B, go, s);
     if (e != hipSuccess) return e;
-    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, lw, oo, s);
+    return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, H.rc, H.c_rc, oo, s);
   }
   return launch_g<false>(P, B, x0, ul, xr, hs, uo, xo, st, its, nullptr, nullptr, gws, nullptr, nullptr, B, oo, s);
 }

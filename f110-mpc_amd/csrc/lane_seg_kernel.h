@@ -637,10 +637,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   const float nanv = __int_as_float(0x7fc00000);
   float* uo = uout + (size_t)b * 2 * N;
   float* xo = xout + (size_t)b * 3 * (N + 1);
-  // SCR with an early GI (f110qp_kernels.hip): the QPs it owns get no outputs from this kernel
-  bool wr = true;
-  if constexpr (SCR) wr = !(oo.scr_skip && oo.scr_skip[b]);
-  if (qowner && wr) {
+  if (qowner) {
     xo[0] = solved ? fX0 : nanv;
     xo[1] = solved ? fY0 : nanv;
     xo[2] = solved ? fTH0 : nanv;
@@ -693,7 +690,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         nviol += !(ta0 + tb0 + gc0 >= 1e-6 * (1.0 + fabs(ta0) + fabs(tb0) + fabs(gc0)));
         nviol += !(ta1 + tb1 + gc1 >= 1e-6 * (1.0 + fabs(ta1) + fabs(tb1) + fabs(gc1)));
       }
-      if (owner && wr) {
+      if (owner) {
         uo[2 * i] = solved ? (float)u0 : nanv;
         uo[2 * i + 1] = solved ? (float)u1 : nanv;
         const double ox = ROT ? cs * x0 - sn * x1 : x0, oy = ROT ? sn * x0 + cs * x1 : x1;
@@ -712,8 +709,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     }
     const double Cu = 0.5 * (double)N * (r0 * ud0 * ud0 + r1 * ud1 * ud1);
     const double dnan = __longlong_as_double(0x7ff8000000000000ll);
-    if (qowner && wr && oo.cost) oo.cost[b] = solved ? J : dnan;
-    if (qowner && wr && oo.obj) oo.obj[b] = solved ? J - Cr - Cu : dnan;
+    if (qowner && oo.cost) oo.cost[b] = solved ? J : dnan;
+    if (qowner && oo.obj) oo.obj[b] = solved ? J - Cr - Cu : dnan;
   }
   if constexpr (SCR) {
     // the QP's violation count over its S lanes; GI priority 1 + count (the list is ordered by it,
@@ -721,9 +718,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
 #pragma unroll
     for (int k = L; k < 64; k <<= 1) nviol += __shfl_xor(nviol, k, 64);
     const bool ok0 = (ga0 * X0 + gb0 * Y0 >= -gc0 - 1e-9) & (ga1 * X0 + gb1 * Y0 >= -gc1 - 1e-9);
-    if (qowner) oo.scr_prio[b] = !wr ? 0 : ((!solved || !ok0) ? 1 : (nviol > 0 ? 1 + nviol : 0));
+    if (qowner) oo.scr_prio[b] = (!solved || !ok0) ? 1 : (nviol > 0 ? 1 + nviol : 0);
   }
-  if (qowner && wr) {
+  if (qowner) {
     status_out[b] = bad ? F110QP_NUMERICAL_ID : (done ? F110QP_SOLVED_ID : F110QP_MAX_ITER_ID);
     if (iters_out) iters_out[b] = bad ? 0 : (done ? iters : max_pass);
   }

@@ -320,7 +320,7 @@ struct Smem {
   double rx[VN], ry[VN];           // recentred reference of the variable's stage (fp64: x_ref - x0
                                    // of two floats is not always a float)
   float rth[VN];
-  float cmult[3 * VN];             // multiplier per constraint id
+  double cmult[3 * VN];            // multiplier per constraint id (fp64: the refinement's)
   alignas(16) float prow[NUM];     // box PDAS: pivot row of T broadcast (pivot_T)
   alignas(16) float yb[NUM];       // box PDAS: right-hand side broadcast (matvec_T)
   double d64[VN];
@@ -678,6 +678,18 @@ __device__ __forceinline__ void matvec_T(Smem<NUM, GAP>& sm, const float (&h)[R]
 // dt = 0.01, so up to four, stopping once the fp32 correction is at its noise level.
 constexpr int kRefineSteps = 4;
 constexpr float kRefineTol = 2e-6f;
+// GI's final point (gap rows): refined until its fp64 KKT residual certifies it (at most
+// kRefineMax residual evaluations), then certified by strong convexity. For a point u that
+// satisfies every row (fp64, 1e-9 relative) and holds its active rows at equality, with
+// rho = H u + g - N_A mu+ (multipliers clamped at 0) and the optimum u*, e = u - u* has
+// e'He <= rho'e <= |rho|_W |e|_H (W = H^-1), so |e|_2 <= |e|_H / sqrt(lambda) <= |rho|_W / sqrt(lambda)
+// with lambda = min(r) <= lambda_min(H) (H = R + Gamma'Q Gamma). SOLVED when
+// rho'W rho <= lambda (kCertTauW max(1, |u|_inf))^2; the W-norm keeps the bound at sqrt(kappa(H))
+// times the rounding of an exact point, where |rho|_2 / lambda would be kappa times (stiff QPs,
+// kappa ~ 4e5 at N = 48, dt = 0.05). Anything else is SOLVED_INACCURATE and goes to the fp64
+// re-check (gi64_kernel.h).
+constexpr int kRefineMax = 8;
+constexpr double kCertTauW = 1e-6;
 // box path's fp64 PDAS (step 4a'): passes, HIK passes before the least-index rule, flips pivoted
 // in place before T is rebuilt, refinement steps and tolerance per pass
 constexpr int kHikPasses = 8;
@@ -688,8 +700,6 @@ constexpr float kRobTight = 1e-14f;  // keep going to fp64 level: the multiplier
                                      // carry ||H_AF|| times the error left in u_F
 template <int NUM>
 constexpr int kRobPasses = kHikPasses + NUM;
-// GI's final check: an active row's multiplier below -kMultTol (1 + max|g|) is a wrong set
-constexpr double kMultTol = 1e-4;
 
 template <int NUM, bool GAP>
 __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const KParams& P,
@@ -1116,15 +1126,6 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   int forced_p = -1;     // violated row found by the fp64 re-check
   float forced_sp = 0.f;
   bool inexact = false;  // GI's final check failed: SOLVED_INACCURATE
-  float gmax = 0.f;      // max |g| (scale of the multiplier tolerances)
-#pragma unroll
-  for (int r = 0; r < R; r++) gmax = fmaxf(gmax, valid[r] ? fabsf(sm.vec[vv[r]]) : 0.f);
-  {
-    int dummy = 0;
-    gmax = -gmax;
-    wave_argmin(gmax, dummy);
-    gmax = -gmax;
-  }
 
   // ---- box rows: fp64 machinery of steps 4a' and 6 (T, its set, the fp64 point) ----------
   float dg[R], ed[R];   // exact diagonal of T / offset of its register copy (pivot_T)
@@ -1490,70 +1491,116 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         p = bid_w;
         sp = readlane_f(sraw_w, (bid_w / 3) & 63);
       } else {
-        // ---- 5. refinement in fp64 + exact feasibility re-check ----
+        // ---- 5. refinement in fp64, feasibility re-check, certificate ----
+        // Newton steps on the equality KKT system of the final set (fp64 residuals, corrections
+        // through the fp32 W and factor; the multipliers kept in fp64 in sm.cmult) until the fp64
+        // residual certifies the point (kRefineMax, kCertTauW), then every inactive row in fp64.
         STAMP(t_ref0);
 #pragma unroll
         for (int r = 0; r < R; r++) {
-          sm.cmult[3 * vv[r]] = 0.f;
-          sm.cmult[3 * vv[r] + 1] = 0.f;
-          sm.cmult[3 * vv[r] + 2] = 0.f;
+          sm.cmult[3 * vv[r]] = 0.0;
+          sm.cmult[3 * vv[r] + 1] = 0.0;
+          sm.cmult[3 * vv[r] + 2] = 0.0;
         }
         wsync();
+        float umaxf = 0.f;
 #pragma unroll
         for (int r = 0; r < R; r++) {
-          if (64 * r + lane < q) sm.cmult[slot_id[r]] = mult[r];
+          if (64 * r + lane < q) sm.cmult[slot_id[r]] = (double)mult[r];
           u64[r] = valid[r] ? (double)xv[r] : 0.0;
+          umaxf = fmaxf(umaxf, valid[r] ? fabsf(xv[r]) : 0.f);
         }
+        {
+          int dummy = 0;
+          umaxf = -umaxf;
+          wave_argmin(umaxf, dummy);
+          umaxf = -umaxf;
+        }
+        const double ctol = kCertTauW * fmax(1.0, (double)umaxf);
+        const double thr2 = fmin(P.r[0], P.r[1]) * ctol * ctol;  // bound on rho'W rho
         const Lin M = sm.M;
         double rxd[R], ryd[R], rthd[R];
 #pragma unroll
         for (int r = 0; r < R; r++) { rxd[r] = sm.rx[vv[r]]; ryd[r] = sm.ry[vv[r]]; rthd[r] = sm.rth[vv[r]]; }
         double px[R], py[R], th[R];
-        bool gi_ref_ok = false;
-        for (int rs = 0; rs < kRefineSteps; rs++) {
-          wsync();
+        // r1 = H u + g - N_A mu at u64 (fp64 rollout and costate), mu from sm.cmult (clamped at 0
+        // with `clamp`); px / py / th the rollout of u64
+        auto kkt_res = [&](bool clamp, double (&r1)[R]) __attribute__((always_inline)) {
           rollout_f64<R>(M, lane, u64, px, py, th);
           double gmx[R], gmy[R];  // gap multipliers of the variable's stage (sides 0,1)
 #pragma unroll
           for (int r = 0; r < R; r++) {
             gmx[r] = 0.0; gmy[r] = 0.0;
             if (GAP) {
-              const double m0 = (double)sm.cmult[3 * (vv[r] & ~1) + 2];
-              const double m1 = (double)sm.cmult[3 * (vv[r] | 1) + 2];
+              double m0 = sm.cmult[3 * (vv[r] & ~1) + 2], m1 = sm.cmult[3 * (vv[r] | 1) + 2];
+              if (clamp) { m0 = fmax(m0, 0.0); m1 = fmax(m1, 0.0); }
               gmx[r] = m0 * ga0 + m1 * ga1;
               gmy[r] = m0 * gb0 + m1 * gb1;
             }
           }
-          double r1[R];
           grad_f64<R>(M, P, lane, N, u64, px, py, th, rxd, ryd, rthd, gmx, gmy, r1);
 #pragma unroll
           for (int r = 0; r < R; r++) {
-            r1[r] = valid[r] ? r1[r] : 0.0;
-            if (valid[r]) r1[r] += -(double)sm.cmult[3 * vv[r]] + (double)sm.cmult[3 * vv[r] + 1];
+            double ml = sm.cmult[3 * vv[r]], mu = sm.cmult[3 * vv[r] + 1];
+            if (clamp) { ml = fmax(ml, 0.0); mu = fmax(mu, 0.0); }
+            r1[r] = valid[r] ? r1[r] - ml + mu : 0.0;
+          }
+        };
+        bool gi_ref_ok = false;
+        float prev = 3.0e38f;
+        for (int rs = 0; rs < kRefineMax; rs++) {
+          wsync();
+          double r1[R];
+          kkt_res(false, r1);
+#pragma unroll
+          for (int r = 0; r < R; r++) {
             sm.d64[vv[r]] = u64[r];
             if (GAP && a == 1 && kk[r] < N) { sm.sx64[kk[r] + 1] = px[r]; sm.sy64[kk[r] + 1] = py[r]; }
             sm.vec[vv[r]] = (float)r1[r];
           }
           wsync();
-          // r2_j = n_j'u - b_j on the active rows (fp64)
-          float r2[R];
+          // w1 = W r1 (the correction's first product) and the residual's W-norm r1'W r1
+          float w1[R];
+          matvec_W<NUM, GAP, R>(sm, lane, w1);
+          double rsq = 0.0;
+#pragma unroll
+          for (int r = 0; r < R; r++) rsq += valid[r] ? r1[r] * (double)w1[r] : 0.0;
+          rsq = wave_sum(rsq);
+          // r2_j = n_j'u - b_j on the active rows (fp64); active rows must hold with equality
+          float r2[R], r2n = 0.f;
 #pragma unroll
           for (int r = 0; r < R; r++) {
             r2[r] = 0.f;
             if (64 * r + lane < q) {
               const int owner = slot_id[r] / 3, t = slot_id[r] - 3 * owner;
-              if (t == 0) r2[r] = (float)(sm.d64[owner] - (double)((owner & 1) ? umin1 : umin0));
-              else if (t == 1) r2[r] = (float)((double)((owner & 1) ? umax1 : umax0) - sm.d64[owner]);
-              else {
+              double r2d, sc;
+              if (t == 0) {
+                const double bd = (double)((owner & 1) ? umin1 : umin0);
+                r2d = sm.d64[owner] - bd;
+                sc = 1.0 + fabs(bd);
+              } else if (t == 1) {
+                const double bd = (double)((owner & 1) ? umax1 : umax0);
+                r2d = bd - sm.d64[owner];
+                sc = 1.0 + fabs(bd);
+              } else {
                 const int st = (owner >> 1) + 1;
-                r2[r] = (owner & 1) ? (float)((double)ga1 * sm.sx64[st] + (double)gb1 * sm.sy64[st] - gbeta1)
-                                    : (float)((double)ga0 * sm.sx64[st] + (double)gb0 * sm.sy64[st] - gbeta0);
+                r2d = (owner & 1) ? ((double)ga1 * sm.sx64[st] + (double)gb1 * sm.sy64[st] - gbeta1)
+                                  : ((double)ga0 * sm.sx64[st] + (double)gb0 * sm.sy64[st] - gbeta0);
+                sc = (double)gnorm;
               }
+              r2[r] = (float)r2d;
+              r2n = fmaxf(r2n, (float)(fabs(r2d) / sc));
             }
           }
-          // w1 = W r1 ; v1_j = n_j' w1
-          float w1[R];
-          matvec_W<NUM, GAP, R>(sm, lane, w1);
+          {
+            int dummy = 0;
+            r2n = -r2n;
+            wave_argmin(r2n, dummy);
+            r2n = -r2n;
+          }
+          if (rsq <= 0.25 * thr2 && r2n <= 1e-9f) { gi_ref_ok = true; break; }
+          if (rs + 1 == kRefineMax) break;
+          // v1_j = n_j' w1
 #pragma unroll
           for (int r = 0; r < R; r++) sm.vec2[vv[r]] = w1[r];
           if (GAP) {
@@ -1602,20 +1649,23 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #pragma unroll
           for (int r = 0; r < R; r++) {
             if (valid[r]) u64[r] += (double)dx[r];
-            mult[r] += du[r];
             adx = fmaxf(adx, valid[r] ? fabsf(dx[r]) : 0.f);
           }
           wsync();
 #pragma unroll
           for (int r = 0; r < R; r++)
-            if (64 * r + lane < q) sm.cmult[slot_id[r]] = mult[r];
-          // a second step only if the first correction was not already at fp32 noise level
+            if (64 * r + lane < q) sm.cmult[slot_id[r]] += (double)du[r];
           int dummy = 0;
           adx = -adx;
           wave_argmin(adx, dummy);  // -max |dx|
-          if (-adx <= kRefineTol) { gi_ref_ok = true; break; }
+          adx = -adx;
+          if (rs >= 2 && !(adx < 0.5f * prev)) break;  // stalled: not certifiable here
+          prev = adx;
         }
         wsync();
+#pragma unroll
+        for (int r = 0; r < R; r++)
+          if (64 * r + lane < q) mult[r] = (float)sm.cmult[slot_id[r]];
         // fp64 feasibility check of every inactive row at the refined point
         rollout_f64<R>(M, lane, u64, px, py, th);
         float best64 = 0.f, sp64 = 0.f;
@@ -1639,14 +1689,28 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         wave_argmin(best64, bid64);
         STAMP_ACC(acc_refine, t_ref0);
         if (bid64 == 0x7fffffff || reentries >= 4) {
-          // final check: the refinement converged, no row violated, no multiplier of the wrong
-          // sign; otherwise the point is reported as SOLVED_INACCURATE
-          float mneg = 0.f;
+          // certificate: refined to the residual bound, every row holds; a negative multiplier
+          // enters clamped at 0 (its row's pull stays in the residual, in primal units / lambda)
+          bool cert = gi_ref_ok && bid64 == 0x7fffffff;
+          bool neg = false;
 #pragma unroll
-          for (int r = 0; r < R; r++) mneg = fminf(mneg, (64 * r + lane < q) ? mult[r] : 0.f);
-          int dummy = 0;
-          wave_argmin(mneg, dummy);
-          inexact = !gi_ref_ok || bid64 != 0x7fffffff || !((double)mneg >= -kMultTol * (1.0 + (double)gmax));
+          for (int r = 0; r < R; r++) neg = neg || (64 * r + lane < q && sm.cmult[slot_id[r]] < 0.0);
+          if (cert && __ballot(neg) != 0ull) {
+            double r1c[R];
+            kkt_res(true, r1c);
+            wsync();
+#pragma unroll
+            for (int r = 0; r < R; r++) sm.vec[vv[r]] = (float)r1c[r];
+            wsync();
+            float wc[R];
+            matvec_W<NUM, GAP, R>(sm, lane, wc);
+            double rsq = 0.0;
+#pragma unroll
+            for (int r = 0; r < R; r++) rsq += valid[r] ? r1c[r] * (double)wc[r] : 0.0;
+            rsq = wave_sum(rsq);
+            cert = rsq <= thr2;
+          }
+          inexact = !cert;
           final_ok = true;
           break;
         }
@@ -1926,7 +1990,10 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   if (lane == 0) {
     status_out[b] = status;
     if (iters_out) iters_out[b] = it;
-    if (oo.rc_list && status != F110QP_SOLVED_ID) oo.rc_list[atomicAdd(oo.rc_count, 1)] = b;  // re-check
+    // re-check list: every answer GI did not certify (an uncertified point, its cap, an
+    // infeasibility found by the fp32 GI); non-finite data and a violated stage-0 row are exact
+    if (oo.rc_list && status != F110QP_SOLVED_ID && !numerical && !infeasible0)
+      oo.rc_list[atomicAdd(oo.rc_count, 1)] = b;
   }
   if (ws.act != nullptr && !grp && Hdbg == nullptr) {
 #pragma unroll

@@ -176,15 +176,20 @@ def test_auto_backend_grouped_policy(capi):
 
 def test_gap_screen_policy(capi):
     """Gap rows under AUTO take the box screen on the lane back end from F110QP_GAP_SCREEN_MIN_BATCH
-    QPs (ungrouped, no warm start); an explicit back end never does. Mirrored by capi.auto_gap_screen."""
+    QPs (ungrouped, no warm start); an explicit LANE back end at every batch size (no warm start),
+    an explicit WAVE back end never. Mirrored by capi.auto_gap_screen."""
     sg = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE))
     for B in (1, 512, 1023, 1024, 4096, 65536):
         assert sg.gap_screen(B) == capi.auto_gap_screen(B) == (B >= capi.GAP_SCREEN_MIN_BATCH), B
     sg.close()
-    for over in (dict(backend=capi.BACKEND_WAVE), dict(backend=capi.BACKEND_LANE), dict(warm_start=1)):
+    for over in (dict(backend=capi.BACKEND_WAVE), dict(warm_start=1),
+                 dict(backend=capi.BACKEND_LANE, warm_start=1)):
         s = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE, **over))
         assert not s.gap_screen(4096), over
         s.close()
+    s = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE, backend=capi.BACKEND_LANE))
+    assert all(s.gap_screen(B) for B in (1, 64, 4096, 65536))
+    s.close()
     s = capi.Solver(capi.default_config(20))  # box rows: nothing to screen
     assert not s.gap_screen(4096)
     s.close()
@@ -199,8 +204,8 @@ def test_qp_dims_match_reference_sizes(capi, oracle):
 
 def test_backend_info_resolves_auto_and_scratch(capi):
     """f110qp_backend_info (host only, no device needed): AUTO resolves to the lane back end at
-    the measured thresholds (F110QP_LANE_MIN_BATCH[_WIDE]), gap rows always to the wave back end
-    (an explicit F110QP_BACKEND_LANE runs the interior point where it fits);
+    the measured thresholds (F110QP_LANE_MIN_BATCH[_WIDE]), gap rows to the wave back end (an
+    explicit F110QP_BACKEND_LANE reports the box screen's lane solve);
     the lane QPs-per-wave fill <= 256 waves; the scratch sits in LDS (fp64 when it fits) while the
     grid's waves are resident with it and in HBM (fp32) at the C4 size."""
     s20 = capi.Solver(capi.default_config(20))
@@ -234,7 +239,7 @@ def test_backend_info_resolves_auto_and_scratch(capi):
     assert sg.backend_info(65536)[0] == capi.BACKEND_WAVE and sg.backend_info(4096)[0] == capi.BACKEND_WAVE
     sl = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE, backend=capi.BACKEND_LANE))
     assert sl.backend_info(4096) == (capi.BACKEND_LANE, 16, 1) and sl.lane_segments(4096) == 4
-    assert sl.backend_info(65536)[0] == capi.BACKEND_WAVE  # the interior point's LDS does not fit
+    assert sl.backend_info(65536) == (capi.BACKEND_LANE, 64, 4)  # the box solve's sequential kernel
     sl.close()
     for s in (s20, s40, sg):
         s.close()

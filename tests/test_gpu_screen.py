@@ -9,6 +9,7 @@ import pytest
 from test_gpu_parity import check, halfspaces_oracle, rel_err
 
 from f110qp import workload
+from fuzz_cases import screen_fuzz_case
 
 pytestmark = pytest.mark.gpu
 
@@ -82,76 +83,67 @@ def test_screen_infeasible_and_non_finite(oracle, capi, monkeypatch):
     np.testing.assert_array_equal(st, out["wave"][2])
 
 
-def test_early_gi_matches_screen_without_it(oracle, capi, monkeypatch):
-    """The early GI (predicted-heaviest QPs on the aux stream, concurrently with the box solve)
-    changes only when GI starts: the same statuses and optimum as the screen without it
-    (F110QP_GAP_EARLY=0), both against the oracle; a small K forces both GI launches to share
-    the batch and the re-check list."""
-    N, B = 20, 2048
-    w, hs = _gap_batch(oracle, B, N, 333, lateral=0.8)
-    out = {}
-    for name, k in (("off", "0"), ("k16", "16"), ("default", None)):
-        if k is None:
-            monkeypatch.delenv("F110QP_GAP_EARLY", raising=False)
-        else:
-            monkeypatch.setenv("F110QP_GAP_EARLY", k)
-        out[name] = check(oracle, capi, N, w, hs, gap=True)
-    for name in ("k16", "default"):
-        np.testing.assert_array_equal(out[name][2], out["off"][2])
-        ok = out["off"][2] == capi.SOLVED
-        assert rel_err(out[name][0][ok], out["off"][0][ok].astype(np.float64)).max() <= 1e-6
-
-
-# Known gaps at the stiff corner dt = 0.05 (DESIGN.md 2h), not of the screen (the explicit wave
-# back end gives the same answers; tools/screen_case_probe.py SEED CASE):
-#   (1, 1) N = 33, q = (10, 17, 0), steering u_des on its upper bound, 1,562 QPs: the wave kernel's
-#          GI returns SOLVED for ~6% of the batch with errors up to 3e-2 after 118-214 iterations;
-#   (2, 1) N = 48, q = (40, 40, 3), u_des on both lower bounds, 1,283 QPs: 3 QPs the oracle solves
-#          stay SOLVED_INACCURATE (GI uncertified, the fp64 re-check does not polish them).
-# Kept visible as strict xfails.
-FUZZ_KNOWN_GAP = {(1, 1), (2, 1)}
-
-
+# The stiff corners at dt = 0.05 (round 4's strict xfails, now plain cases): (1, 1) N = 33,
+# q = (10, 17, 0), steering u_des on its upper bound, where the wave kernel's fp32 GI ended at wrong
+# points its old multiplier test let through; (2, 1) N = 48, q = (40, 40, 3), u_des on both lower
+# bounds, where it could not certify three QPs. The fp64 certificate sends both kinds to the fp64
+# GI re-check (gi64_kernel.h).
 @pytest.mark.parametrize("seed,case", [(s, c) for s in range(3) for c in range(2)])
-def test_screen_fuzz_configs_against_oracle(oracle, capi, seed, case, request):
-    if (seed, case) in FUZZ_KNOWN_GAP:
-        request.applymarker(pytest.mark.xfail(strict=True, reason="stiff-corner GI accuracy gap, DESIGN.md 2h"))
+def test_screen_fuzz_configs_against_oracle(oracle, capi, seed, case):
     """The AUTO gap path at screen sizes (1,024..1,600 QPs) over random corners of the ABI's
     parameter space (horizon, dt, weights incl. zero state weights, u_des on a bound, narrow
     bounds): exact status parity with the oracle (QPs it cannot certify excluded, as in
     test_gpu_parity.test_fuzz_configs_against_oracle), the optimum and objective to tolerance."""
-    rng = np.random.default_rng(7100 + seed)
-    for c in range(case + 1):
-        N = int(rng.choice([5, 13, 20, 27, 33, 40, 48]))
-        lo0, lo1 = float(rng.uniform(1.0, 3.5)), float(rng.uniform(-0.6, -0.1))
-        hi0, hi1 = lo0 + float(rng.uniform(0.3, 2.0)), -lo1 * float(rng.uniform(0.5, 1.5))
-        ud = [float(rng.choice([hi0, lo0, 0.5 * (lo0 + hi0)])), float(rng.choice([0.0, hi1, lo1]))]
-        q01 = float(rng.choice([0.0, 1.0, 10.0, 40.0]))
-        over = dict(q=[q01, q01 if rng.random() < 0.5 else float(rng.uniform(0.5, 20.0)),
-                       float(rng.choice([0.0, 0.5, 3.0]))],
-                    r=[float(rng.uniform(0.05, 2.0)), float(rng.uniform(0.5, 10.0))], u_des=ud,
-                    u_min=[lo0, lo1], u_max=[hi0, hi1])
-        dt = float(np.float32(rng.choice([0.005, 0.01, 0.02, 0.05])))
-        B = int(rng.integers(1024, 1600))
-        w = workload.make_batch(B, N, seed=int(rng.integers(1 << 30)), heading="true",
-                                lateral=float(rng.uniform(0.0, 1.5)), steer_range=float(rng.uniform(0.0, 0.8)))
-        ranges, amin, ainc, amax = workload.make_scans(B, seed=int(rng.integers(1 << 30)))
-        if c < case:
-            continue
-        hs = halfspaces_oracle(oracle, w["x0"], ranges, (amin, ainc, amax))
-        s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE, dt=dt, **over))
-        assert s.gap_screen(B)
-        u, x, st, it, ob, co = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs, objective=True)
-        s.close()
-        prm = oracle.params(N, dt=dt, **over)
-        ur, xr, sr, obr = oracle.solve_batch(prm, w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=True,
-                                             objective=True)
-        tag = (seed, case, N, dt, B, over)
-        cmp = sr != oracle.UNCERTIFIED
-        assert (sr == oracle.UNCERTIFIED).sum() <= max(1, 0.02 * B), tag
-        np.testing.assert_array_equal(st[cmp], sr[cmp], err_msg=str(tag))
-        ok = sr == oracle.SOLVED
-        if ok.any():
-            assert rel_err(u[ok], ur[ok]).max() <= 1e-4, tag
-            assert rel_err(x[ok], xr[ok]).max() <= 1e-4, tag
-            np.testing.assert_allclose(ob[ok], obr[ok], rtol=1e-6, atol=1e-6, err_msg=str(tag))
+    N, dt, B, over, w, ranges, geom = screen_fuzz_case(seed, case)
+    hs = halfspaces_oracle(oracle, w["x0"], ranges, geom)
+    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE, dt=dt, **over))
+    assert s.gap_screen(B)
+    u, x, st, it, ob, co = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs, objective=True)
+    s.close()
+    prm = oracle.params(N, dt=dt, **over)
+    ur, xr, sr, obr = oracle.solve_batch(prm, w["x0"], w["u_lin"], w["x_ref"], hs, gap_active=True,
+                                         objective=True)
+    tag = (seed, case, N, dt, B, over)
+    cmp = sr != oracle.UNCERTIFIED
+    assert (sr == oracle.UNCERTIFIED).sum() <= max(1, 0.02 * B), tag
+    np.testing.assert_array_equal(st[cmp], sr[cmp], err_msg=str(tag))
+    ok = sr == oracle.SOLVED
+    if ok.any():
+        assert rel_err(u[ok], ur[ok]).max() <= 1e-4, tag
+        assert rel_err(x[ok], xr[ok]).max() <= 1e-4, tag
+        np.testing.assert_allclose(ob[ok], obr[ok], rtol=1e-6, atol=1e-6, err_msg=str(tag))
+
+
+@pytest.mark.parametrize("backend", ["auto", "wave"])
+def test_recheck_processes_every_listed_qp(oracle, capi, backend):
+    """More QPs than one re-check grid holds go to the fp64 re-check (4,608 walls the fp32 GI finds
+    infeasible, mixed with feasible ones): every listed QP is re-checked (the grid-stride loop over
+    the device-side count), so the statuses are the oracle's whatever the list order, and two calls
+    agree bit for bit."""
+    from test_oracle import infeasible_cases
+
+    N, B = 20, 5120
+    w = workload.make_batch(B, N, seed=77)
+    x0w, wall = infeasible_cases()[0]
+    hs = np.zeros((B, 2, 3), np.float32)
+    feas = np.arange(B) % 10 == 0  # the wall 1 m ahead: reachable
+    for b in range(B):
+        w["x0"][b] = x0w
+        w["u_lin"][b] = [4.5, 0.0]
+        hs[b] = wall
+        if feas[b]:
+            hs[b, :, 2] = x0w[0] + 1.0
+    be = {"auto": capi.BACKEND_AUTO, "wave": capi.BACKEND_WAVE}[backend]
+    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE, backend=be))
+    u1, x1, st1, _ = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
+    u2, x2, st2, _ = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs)
+    s.close()
+    assert (st1[~feas] == capi.PRIMAL_INFEASIBLE).all()
+    np.testing.assert_array_equal(st1, st2)
+    np.testing.assert_array_equal(np.nan_to_num(u1, nan=7.0), np.nan_to_num(u2, nan=7.0))
+    idx = np.r_[np.where(feas)[0][:32], np.where(~feas)[0][:32]]
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx], hs[idx],
+                                    gap_active=True)
+    np.testing.assert_array_equal(st1[idx], sr)
+    ok = sr == oracle.SOLVED
+    assert rel_err(u1[idx][ok], ur[ok]).max() <= 1e-4
