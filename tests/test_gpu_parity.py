@@ -5,6 +5,7 @@ Tolerance (north star: match the QP's primal solution to 1e-4 rel-tol): for ever
 against the exact optimum u* of the reference QP (oracle/f110_oracle.c, KKT-certified), plus
 identical per-QP status. In practice the kernel lands at fp32 output rounding (~1e-7).
 """
+import json
 import os
 
 import numpy as np
@@ -58,7 +59,8 @@ def test_golden_fixtures(capi, name):
     d = np.load(os.path.join(GOLDEN, name + ".npz"))
     N = int(d["horizon"])
     gap = bool(d["gap"])
-    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE))
+    over = json.loads(str(d["params"])) if "params" in d.files else {}  # stiff-corner fixtures
+    s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE, **over))
     u, x, st, _ = s.solve(d["x0"], d["u_lin"], d["x_ref"], d["halfspace"] if gap else None)
     s.close()
     np.testing.assert_array_equal(st, d["status"])
