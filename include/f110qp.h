@@ -67,12 +67,13 @@ extern "C" {
 
 /* per-QP status codes (values follow OSQP's status ids) */
 #define F110QP_SOLVED 1
-#define F110QP_SOLVED_INACCURATE 2 /* wave back end: a point whose fp64 KKT check failed and    */
-                                  /* that the fp64 re-check (gap rows: the lane interior point)  */
-                                  /* could not certify either: u, x, obj, cost are written but   */
-                                  /* not certified, and f110qp_select_dev never picks it. Its    */
-                                  /* active set may seed the next warm start (a seed is only a   */
-                                  /* first guess; every solve is certified on its own).          */
+#define F110QP_SOLVED_INACCURATE 2 /* a point whose fp64 certificate failed (box rows: the KKT  */
+                                  /* check in primal units; gap rows: strong convexity, also    */
+                                  /* after the fp64 Goldfarb-Idnani re-check): u, x, obj, cost  */
+                                  /* are written but not certified, and f110qp_select_dev never */
+                                  /* picks it. Its active set may seed the next warm start (a   */
+                                  /* seed is only a first guess; every solve is certified on    */
+                                  /* its own).                                                  */
 #define F110QP_MAX_ITER -2
 #define F110QP_PRIMAL_INFEASIBLE -3
 #define F110QP_NUMERICAL -10      /* non-finite data or factorisation breakdown */
@@ -87,12 +88,13 @@ extern "C" {
                                   /* F110QP_LANE_MIN_BATCH_WIDE (N > 32)                       */
 #define F110QP_BACKEND_WAVE 1     /* one wavefront per QP: condensed W = H^-1 + PDAS/GI         */
 #define F110QP_BACKEND_LANE 2     /* one lane per QP: Riccati/PDAS in fp64; with gap rows the   */
-                                  /* Riccati interior point (lane_ipm_kernel.h) where its LDS  */
-                                  /* fits (else the wave back end); QPs it does not polish go  */
-                                  /* to the wave kernel's GI in the same call                  */
-/* Gap rows: AUTO keeps the wave back end (C3, 4,096 x N = 20: wave GI 290 us, lane interior point
- * 1,010 us); the wave kernel's gap-row QPs it does not report SOLVED are re-checked
- * in fp64 by the interior point in the same call (KKT-checked polish or a Farkas certificate).
+                                  /* box screen at every batch size: the lane solve of the box- */
+                                  /* only problem, the wave kernel's GI for the QPs whose box   */
+                                  /* optimum violates a gap row (no warm state, ungrouped)      */
+/* Gap rows: the wave kernel's GI (AUTO: behind the box screen from
+ * F110QP_GAP_SCREEN_MIN_BATCH QPs); GI's final point is certified in fp64 by strong convexity, and
+ * every QP it does not certify is re-checked in the same call by an fp64 Goldfarb-Idnani with the
+ * oracle's rules (SOLVED, PRIMAL_INFEASIBLE, MAX_ITER or SOLVED_INACCURATE from there).
  * AUTO thresholds, measured on MI355X (kernel us, DESIGN.md section 6, round 3: the lane back end
  * with the partitioned-horizon kernel below one wave per SIMD, the wave back end with its fp64
  * certification). N = 20 (C2 recipe, cold): wave 27.3 vs lane 30.6 at 512 (before the last
@@ -224,13 +226,14 @@ int f110qp_select_dev(int batch, const int* group, int num_groups, const double*
  * points): backend = F110QP_BACKEND_WAVE or _LANE (what AUTO resolves to), qps_per_wave (lane:
  * QPs per 64-lane wavefront; wave: 1) and scratch (lane: 1 LDS fp64, 2 LDS fp32, 3 HBM fp64,
  * 4 HBM fp32 Riccati gain scratch; the partitioned-horizon kernel uses 1 or 2 (float references
- * and scratch where fp64 does not fit), the interior point 1; wave: 0). Any pointer may be NULL. */
+ * and scratch where fp64 does not fit); wave: 0). With gap rows, LANE means the box screen's lane
+ * solve (F110QP_BACKEND_LANE). Any pointer may be NULL. */
 int f110qp_backend_info(f110qp_ctx* ctx, int batch, int grouped, int* backend, int* qps_per_wave,
                         int* scratch);
 
 /* Horizon segments per QP of that launch: 1, or S = 2 / 4 / 8 when the lane back end splits each
  * QP's horizon over S lanes (partitioned Riccati; batches too small to give every SIMD a wave of
- * distinct QPs; with gap rows on the lane back end the interior point's S = 2..16).
+ * distinct QPs; with gap rows on the lane back end: the box screen's solve).
  * The result is the exact optimum either way. */
 int f110qp_lane_segments(f110qp_ctx* ctx, int batch, int* segments);
 
