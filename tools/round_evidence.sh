@@ -1,5 +1,5 @@
 # Round evidence on one MI355X (profiles/<round>/): the -m gpu suite, smoke(), one bench line per
-# BASELINE config (+ the C4 shard sizes of 2/4/8 GPUs and the C3 interior-point line), rocprofv3
+# BASELINE config (+ the C4 shard sizes of 2/4/8 GPUs), rocprofv3
 # kernel stats + FETCH_SIZE / WRITE_SIZE passes of the dominant kernel (tools/profile_round.sh),
 # SQ counter passes (tools/sq_pass.sh) and a 2-rank rehearsal of the multi-process bench.
 # Usage (repo root, on the GPU box): bash tools/round_evidence.sh r04 [part]
@@ -7,7 +7,7 @@
 #   python tools/summarize_profiles.py r04 c2 c3 c4 c5 c2_big c4_8192 c4_16384
 #   python tools/summarize_sq.py r04 c2:lane_seg_kernel c4_8192:lane_seg_kernel c4_16384:lane_seg_kernel c3:solve_kernel
 set -o pipefail
-rnd=${1:-r04}
+rnd=${1:-r05}
 part=${2:-all}
 out=gpurun_out/$rnd
 mkdir -p $out
@@ -24,7 +24,6 @@ if [ $part = bench ] || [ $part = all ]; then
 b default
 b c2 --config c2 --no-cpu
 b c3 --config c3 --no-cpu
-b c3_ipm --config c3 --no-cpu --no-latency --backend lane
 b c4 --config c4 --no-cpu
 b c4_shard8192 --config c4 --batch 8192 --no-cpu --no-latency
 b c4_shard16384 --config c4 --batch 16384 --no-cpu --no-latency
@@ -43,9 +42,9 @@ bash tools/sq_pass.sh c2 --config c2 || exit 9
 bash tools/sq_pass.sh c4_8192 --config c4 --batch 8192 || exit 9
 bash tools/sq_pass.sh c4_16384 --config c4 --batch 16384 || exit 9
 bash tools/sq_pass.sh c3 --config c3 || exit 9
-for c in c2 c4; do
-  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29517 \
-    bench.py --gpus 2 --config $c --dist-backend gloo --no-cpu --no-latency --steps 20 2> $out/bench_2rank_$c.err | grep "^{\"metric\"" > $out/bench_2rank_gloo_$c.json || exit 8
+for c in c2 c4; do  # bench.py starts its two ranks itself (gloo: both on GPU 0)
+  timeout -k 10 300 python bench.py --gpus 2 --config $c --dist-backend gloo --no-cpu --no-latency --steps 20 \
+    2> $out/bench_2rank_$c.err | grep "^{\"metric\"" > $out/bench_2rank_gloo_$c.json || exit 8
 done
 fi
 echo evidence done

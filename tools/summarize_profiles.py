@@ -15,7 +15,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"wave": "solve_kernel", "lane": "lane_kernel", "lane_seg": "lane_seg_kernel", "lane_ipm": "lane_ipm_kernel"}
+KERNELS = {"wave": "solve_kernel", "lane": "lane_kernel", "lane_seg": "lane_seg_kernel"}
 
 
 def find(pattern):
@@ -43,9 +43,7 @@ def main():
         base = os.path.join(ROOT, "gpurun_out", f"prof_{c}")
         bench = json.load(open(os.path.join(base, "bench_trace.json")))
         be = "lane" if bench["config"]["backend"].startswith("lane") else "wave"
-        if be == "lane" and bench["config"].get("gap_rows"):
-            be = "lane_ipm"
-        elif be == "lane" and bench["config"].get("lane_segments", 1) > 1:
+        if be == "lane" and bench["config"].get("lane_segments", 1) > 1:
             be = "lane_seg"
         kname = KERNELS[be]
         ks = find(os.path.join(base, "trace", "**", "*kernel_stats.csv"))
