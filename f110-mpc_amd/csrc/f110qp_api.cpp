@@ -94,6 +94,7 @@ struct f110qp_ctx {
   DevBuf din, dout;   // their device copies for batches above kZeroCopyMaxBatch
   DevBuf wW, wkey, wact;  // warm-start slot state (config.warm_start)
   int warm_batch = 0;     // batch size the warm state was laid out for
+  int warm_calls = 0;     // warm calls since the state was laid out (WarmState::call)
   DevBuf gW, gkey, glead;    // grouped mode: W = H^-1, key and leader per group
   DevBuf dgrp;               // host-pointer grouped calls: device copy of the group ids
   DevBuf lscr;               // lane back end: HBM Riccati scratch (when not in LDS)
@@ -253,17 +254,21 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
   const size_t B = (size_t)batch, nu = 2 * (size_t)c->cfg.horizon;
   const size_t rows = (nu + 63) / 64;  // register rows per lane (act masks: 2 x 64 bits per row)
   hipError_t e;
-  if ((e = c->wW.ensure(B * nu * nu * 4)) || (e = c->wkey.ensure(B * 16)) ||
+  // keys (16 B per QP), then the lane back ends' last-hit call (warm_traffic)
+  if ((e = c->wW.ensure(B * nu * nu * 4)) || (e = c->wkey.ensure(B * 16 + 16)) ||
       (e = c->wact.ensure(B * 16 * rows)))
     return hip_fail(e, "hipMalloc warm-start state");
   if (c->warm_batch != batch) {
-    if ((e = hipMemsetAsync(c->wkey.p, 0, B * 16, s)) || (e = hipMemsetAsync(c->wact.p, 0, B * 16 * rows, s)))
+    if ((e = hipMemsetAsync(c->wkey.p, 0, B * 16 + 16, s)) || (e = hipMemsetAsync(c->wact.p, 0, B * 16 * rows, s)))
       return hip_fail(e, "hipMemsetAsync warm-start state");
     c->warm_batch = batch;
+    c->warm_calls = 0;
   }
   ws->W = (float*)c->wW.p;
   ws->key = (unsigned*)c->wkey.p;
   ws->act = (unsigned long long*)c->wact.p;
+  ws->hit_call = (int*)((char*)c->wkey.p + B * 16);
+  ws->call = ++c->warm_calls;
   return F110QP_OK;
 }
 

@@ -45,7 +45,28 @@ struct WarmState {
   unsigned long long* act = nullptr;
   const int* group = nullptr;
   int ngroups = 0;
+  // lane back ends: the context's call counter (from 1) and a device int holding the last call in
+  // which a wave saw a key hit (see warm_traffic)
+  int* hit_call = nullptr;
+  int call = 0;
 };
+
+// Whether a lane-back-end wave moves warm-start traffic in this call (loads its QPs' keys and masks,
+// writes them back). On the closed-loop stream (configs[4]) theta0 changes every tick, so no key
+// ever hits, and that traffic measured 0.7 us per call (0.55 the write-back, 0.15 the key loads:
+// C5 kernel 29.2 against 28.5 cold). It runs while a hit was seen within the last kWarmRecent
+// calls, and on two probe calls in every kWarmProbe (the first writes keys, the second can hit),
+// so a stream whose linearisation points repeat turns it back on within kWarmProbe calls. Without
+// hit_call (grouped / wave paths): always.
+constexpr int kWarmRecent = 2, kWarmProbe = 32;
+__device__ __forceinline__ int warm_last_hit(const WarmState& ws) {  // load early, test late
+  return ws.hit_call ? __builtin_nontemporal_load(ws.hit_call) : 0;
+}
+__device__ __forceinline__ bool warm_traffic(const WarmState& ws, int last) {
+  if (!ws.act || !ws.key) return false;
+  if (!ws.hit_call) return true;
+  return ws.call - last <= kWarmRecent || ws.call % kWarmProbe <= 1;
+}
 
 // LaneWork::hand for a call of B gap-row QPs: kHandInts(B) = 3 B + 4 ints, the two counts first
 // (padded to four ints), then three B-int arrays.

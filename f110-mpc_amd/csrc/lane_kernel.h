@@ -136,6 +136,8 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
   const int b = b0 + slot;
   const int N = P.N;
   const int n3 = 3 * N;
+  const int R = (2 * N + 63) / 64;  // register-row count of the wave kernel's act layout
+  const int wlast = warm_last_hit(ws);  // the warm-start traffic switch (warm_traffic)
 
   // ---- stage the wave's reference paths (nq rows of 3S floats, the first 3N of each used) ---
   // Linear, coalesced sweep over the rows' first 3N entries (element e = q 3N + c -> stg[c L + q],
@@ -175,6 +177,21 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
       }
     }
     __syncthreads();
+  }
+  // warm start: the slot's key and active-set masks when this call moves warm traffic (wlast
+  // arrived with the staging loads); the masks unconditionally, so that no second dependent round
+  // trip follows the key compare
+  const bool wt = warm_traffic(ws, wlast);
+  uint4 wkey = make_uint4(0u, 0u, 0u, 0u);
+  unsigned long long wact[4] = {0ull, 0ull, 0ull, 0ull};
+  if (wt) {
+    wkey = *reinterpret_cast<const uint4*>(ws.key + 4 * (size_t)b);
+    wact[0] = ws.act[2 * R * b];
+    wact[1] = ws.act[2 * R * b + 1];
+    if (R > 1) {
+      wact[2] = ws.act[2 * (R * b + 1)];
+      wact[3] = ws.act[2 * (R * b + 1) + 1];
+    }
   }
   // a non-finite reference entry flags the QP: each lane scans its QP's staged row (~10
   // instructions per entry; a ballot per staged element measured more at C4 and c2_big sizes)
@@ -249,7 +266,6 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
         reinterpret_cast<ST*>(scr) + (size_t)blockIdx.x * N * 8 * L + (size_t)slot * 8, 32));
     ap = reinterpret_cast<int*>(xr_s + (DREF ? 6 : 3) * N * L) + slot;
   }
-  const int R = (2 * N + 63) / 64;  // register-row count of the wave kernel's act layout
   const unsigned kth = __float_as_uint(fTH0), kv = __float_as_uint(ulg[2 * b + 0]);
   const unsigned kd = __float_as_uint(ulg[2 * b + 1]);
   {
@@ -258,20 +274,10 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
     // stale seed measured 1.61 vs 1.49 passes per QP cold. Key valid flag: 1 = written by the
     // wave kernel with its W = H^-1, 2 = by this kernel (act masks only, never a W for the wave
     // kernel to reuse).
-    unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
-    bool hit = false;
-    if (ws.act && ws.key) {
-      const unsigned* key = ws.key + 4 * b;
-      hit = key[3] != 0u && key[0] == kth && key[1] == kv && key[2] == kd;
-    }
-    if (hit) {
-      lo0 = ws.act[2 * R * b];
-      hi0 = ws.act[2 * R * b + 1];
-      if (R > 1) {
-        lo1 = ws.act[2 * (R * b + 1)];
-        hi1 = ws.act[2 * (R * b + 1) + 1];
-      }
-    }
+    const bool hit = wkey.w != 0u && wkey.x == kth && wkey.y == kv && wkey.z == kd;
+    if (ws.hit_call && __ballot(hit) != 0ull && lane == 0) *ws.hit_call = ws.call;
+    const unsigned long long lo0 = hit ? wact[0] : 0ull, hi0 = hit ? wact[1] : 0ull;
+    const unsigned long long lo1 = hit ? wact[2] : 0ull, hi1 = hit ? wact[3] : 0ull;
     // (a cold start from the free set beats seeding the inputs whose u_des sits on a bound:
     // measured +0.5 PDAS passes per QP with the seed on the C2/C4 workloads)
     // stage i's two bits sit at bit 2i of the 128-bit (row 1 : row 0) masks: shifted out two at a
@@ -702,7 +708,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
     if (owner && oo.cost) oo.cost[b] = solved ? J : nanv;
     if (owner && oo.obj) oo.obj[b] = solved ? J - Cr - Cu : nanv;
   }
-  if (owner && ws.act) {  // active set of this solution for the next tick
+  if (owner && wt) {  // active set of this solution for the next tick
     unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
     for (int i = 0; i < N; i++) {
       const unsigned st = (unsigned)ap[i * L];
@@ -722,10 +728,8 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
       ws.act[2 * (R * b + 1)] = lo1;
       ws.act[2 * (R * b + 1) + 1] = hi1;
     }
-    if (ws.key) {
-      unsigned* key = ws.key + 4 * b;
-      key[0] = kth; key[1] = kv; key[2] = kd; key[3] = 2u;
-    }
+    unsigned* key = ws.key + 4 * b;
+    key[0] = kth; key[1] = kv; key[2] = kd; key[3] = 2u;
   }
 #ifdef F110QP_STAMPS
   if (lane == 0 && blockIdx.x < 4096) {

@@ -132,15 +132,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   int* const ap = reinterpret_cast<int*>(lbase + o_ap) + lane;             // [mM][64]
   ST* const sc = reinterpret_cast<ST*>(lbase + o_sc) + lane;               // [mM][NV][64]
 
-  // per-QP inputs and the warm-start key, issued before the staging loads so that both share
-  // one HBM round trip
+  // per-QP inputs and the warm-start traffic switch (warm_traffic), issued before the staging loads
   const float fX0 = x0g[3 * b + 0], fY0 = x0g[3 * b + 1], fTH0 = x0g[3 * b + 2];
   const float fv = ulg[2 * b + 0], fd = ulg[2 * b + 1];
-  unsigned key0 = 0u, key1 = 0u, key2 = 0u, key3 = 0u;
-  if (ws.act && ws.key) {
-    const unsigned* key = ws.key + 4 * b;
-    key0 = key[0]; key1 = key[1]; key2 = key[2]; key3 = key[3];
-  }
+  const int wlast = warm_last_hit(ws);
   // ---- stage the wave's reference paths (float, [3N][L]) into the scratch region ----
   // Element e = q 3N + c of the wave's nq rows (row stride 3 xr_stride in HBM) goes to
   // stg[c L + q]. (q, c) advance by 64 elements per step without a division, every load reads a
@@ -173,6 +168,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       for (int j = 0; j < kChunk; j++) stg[dst[j]] = vbuf[j];
     }
     __syncthreads();
+  }
+  // the warm-start key, when this call moves warm traffic (wlast arrived with the staging loads; the
+  // key's round trip overlaps the linearisation below)
+  const bool wt = warm_traffic(ws, wlast);
+  unsigned key0 = 0u, key1 = 0u, key2 = 0u, key3 = 0u;
+  if (wt) {
+    const uint4 k4 = *reinterpret_cast<const uint4*>(ws.key + 4 * (size_t)b);
+    key0 = k4.x; key1 = k4.y; key2 = k4.z; key3 = k4.w;
   }
 
   SSTAMP(t_stg);
@@ -242,10 +245,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
 #ifdef F110QP_SEG_SEED_ANY  // measurement knob: seed from the slot's previous set on any key
                             // (measured C5 31.2 -> 34.9 us: the stale set costs passes)
-    const bool hit = ws.act && ws.key && key3 != 0u;
+    const bool hit = wt && key3 != 0u;
 #else
-    const bool hit = ws.act && ws.key && key3 != 0u && key0 == kth && key1 == kv && key2 == kd;
+    const bool hit = wt && key3 != 0u && key0 == kth && key1 == kv && key2 == kd;
 #endif
+    if (ws.hit_call && __ballot(hit) != 0ull && lane == 0) *ws.hit_call = ws.call;
     if (hit) {
       lo0 = ws.act[2 * R * b];
       hi0 = ws.act[2 * R * b + 1];
@@ -724,7 +728,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     status_out[b] = bad ? F110QP_NUMERICAL_ID : (done ? F110QP_SOLVED_ID : F110QP_MAX_ITER_ID);
     if (iters_out) iters_out[b] = bad ? 0 : (done ? iters : max_pass);
   }
-  if (ws.act) {  // active set of this solution for the next tick (OR over the segments)
+  if (wt) {  // active set of this solution for the next tick (OR over the segments)
     // the lane's 2m bits (input a of stage t at bit 2t + a), placed at bit 2 s0 of the pair
     unsigned long long lw = 0, hw = 0;
     for (int t = 0; t < m; t++) {
@@ -751,10 +755,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         ws.act[2 * (R * b + 1)] = lo1;
         ws.act[2 * (R * b + 1) + 1] = hi1;
       }
-      if (ws.key) {
-        unsigned* key = ws.key + 4 * b;
-        key[0] = kth; key[1] = kv; key[2] = kd; key[3] = 2u;
-      }
+      unsigned* key = ws.key + 4 * b;
+      key[0] = kth; key[1] = kv; key[2] = kd; key[3] = 2u;
     }
   }
 #ifdef F110QP_STAMPS

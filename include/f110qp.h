@@ -140,6 +140,8 @@ typedef struct {
                     /*    linearisation point (theta0, v, steer) is bit-identical to its    */
                     /*    previous call's, and the previous active set seeds the solve.    */
                     /*    Slot b of call t+1 continues slot b of call t (same batch size). */
+                    /*    The lane back ends move this state only while keys hit (within  */
+                    /*    the last 2 calls, or on 2 probe calls in every 32).             */
   int backend;      /* F110QP_BACKEND_AUTO | _WAVE | _LANE (both give the exact optimum)    */
   int x_ref_points; /* points per QP in x_ref, >= N (0 = N). MPC::Update receives the whole   */
                     /* miniPath and reads its first N states (mpc.cpp:223-228): pass the      */

@@ -897,3 +897,38 @@ def test_fuzz_configs_against_oracle(oracle, capi, seed):
             assert rel_err(u[ok], ur[ok]).max() <= TOL, tag
             assert rel_err(x[ok], xr[ok]).max() <= TOL, tag
             np.testing.assert_allclose(ob[ok], obr[ok], rtol=1e-6, atol=1e-6, err_msg=str(tag))
+
+
+def test_warm_traffic_switches_off_and_back_on(oracle, capi):
+    """The lane back ends' warm write-back (f110qp_kernels.h warm_traffic): on a closed-loop stream
+    no key hits, so after kWarmRecent calls the masks and keys are no longer written (solves are
+    then cold ones); when the linearisation points start to repeat, a probe call (every
+    kWarmProbe = 32) writes them again, the next call hits, and the repeated QP is seeded with its
+    own final active set (one pass, bar degenerate bounds). Every answer exact throughout."""
+    N, B, T = 20, 1024, 6
+    prm = oracle.params(N)
+    ref = []
+
+    def solve(x0, ul, xr):
+        u, x, st = oracle.solve_batch(prm, x0, ul, xr)
+        ref.append((u, x, st))
+        return u
+
+    ticks = workload.closed_loop_stream(solve, B, N, T, seed=77)
+    warm = capi.Solver(capi.default_config(N, warm_start=1))
+    cold = capi.Solver(capi.default_config(N))
+    assert warm.backend_info(B)[0] == capi.BACKEND_LANE
+    for t, w in enumerate(ticks):
+        u, x, st, it = warm.solve(w["x0"], w["u_lin"], w["x_ref"])
+        assert rel_err(u, ref[t][0]).max() <= TOL, t
+        if t >= 3:  # write-back off: the same passes as a cold solve
+            np.testing.assert_array_equal(it, cold.solve(w["x0"], w["u_lin"], w["x_ref"])[3])
+    w = ticks[-1]
+    its = []
+    for k in range(40):  # calls T+1 .. T+40 repeat the last tick: probes at calls 32 and 33
+        u, x, st, it = warm.solve(w["x0"], w["u_lin"], w["x_ref"])
+        assert rel_err(u, ref[-1][0]).max() <= TOL, k
+        its.append(it.mean())
+    warm.close()
+    cold.close()
+    assert its[-1] <= 1.01 and its[-1] < its[0], its
