@@ -243,22 +243,30 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
     c1.warm_start = 0  # a cold solve per call: the latency of one control tick
     c1.x_ref_points = 0
     s1 = capi.Solver(c1)
-    dev_t, prep_t, host_t, batch_t = [], [], [], []
+    dev_t, prep_t, prep_async_t, host_t, batch_t = [], [], [], [], []
     for i in range(reps + 20):
         t0 = time.perf_counter()
         s1.solve_dev(one["x0"], one["u_lin"], one["x_ref"], h1, uo, xo, st, stream=stream)
         stream.synchronize()
         if i >= 20:
             dev_t.append(time.perf_counter() - t0)
-    # the same through the prepared launcher: one C call per tick (what a C++ caller of the ABI
-    # pays), no ctypes argument conversion
+    # the same through the prepared launcher: one C call per tick that returns with the answer
+    # (f110qp_solve_batch_dev_sync: launch, then a busy wait on the stream; what a C++ caller of the
+    # ABI pays), no ctypes argument conversion
+    launch1s = s1.prepare_dev(one["x0"], one["u_lin"], one["x_ref"], h1, uo, xo, st, stream=stream, sync=True)
+    for i in range(reps + 20):
+        t0 = time.perf_counter()
+        launch1s()
+        if i >= 20:
+            prep_t.append(time.perf_counter() - t0)
+    # the asynchronous launcher followed by torch's stream synchronize (round-4 measurement)
     launch1 = s1.prepare_dev(one["x0"], one["u_lin"], one["x_ref"], h1, uo, xo, st, stream=stream)
     for i in range(reps + 20):
         t0 = time.perf_counter()
         launch1()
         stream.synchronize()
         if i >= 20:
-            prep_t.append(time.perf_counter() - t0)
+            prep_async_t.append(time.perf_counter() - t0)
     # the B = 1 kernel alone (HIP events over back-to-back launches)
     ea = torch.cuda.Event(enable_timing=True)
     eb = torch.cuda.Event(enable_timing=True)
@@ -284,13 +292,15 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
         stream.synchronize()
         if i >= 5:
             batch_t.append(time.perf_counter() - t0)
-    return {"single_qp_device": pct(prep_t), "single_qp_device_ctypes": pct(dev_t),
+    return {"single_qp_device": pct(prep_t), "single_qp_device_async_then_sync": pct(prep_async_t),
+            "single_qp_device_ctypes": pct(dev_t),
             "single_qp_host_pointers": pct(host_t), "batch_launch": pct(batch_t),
             "single_qp_kernel_us": k1_us,
             "single_qp_backend": ("lane" + (f" (S = {seg1})" if seg1 > 1 else "")) if be1 == capi.BACKEND_LANE else "wave",
-            "note": "wall clock per call incl. launch + stream sync: single_qp_device through the prepared "
-                    "launcher (one C call), _ctypes with the per-call argument conversion; host-pointer path "
-                    "adds H2D/D2H over PCIe"}
+            "note": "wall clock per call incl. launch + wait for the results: single_qp_device is one C call "
+                    "(f110qp_solve_batch_dev_sync: launch + busy wait on the stream), _async_then_sync the "
+                    "asynchronous launcher then torch's stream synchronize, _ctypes with the per-call argument "
+                    "conversion; host-pointer path adds H2D/D2H over PCIe"}
 
 
 def _halfspaces_host(w, B):

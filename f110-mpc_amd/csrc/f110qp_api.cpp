@@ -345,6 +345,19 @@ int f110qp_solve_batch_dev(f110qp_ctx* c, int batch, const float* x0, const floa
   return f110qp_solve_batch_ex_dev(c, batch, x0, ul, xr, hs, uo, xo, st, it, nullptr, nullptr, stream);
 }
 
+int f110qp_solve_batch_dev_sync(f110qp_ctx* c, int batch, const float* x0, const float* ul,
+                                const float* xr, const float* hs, float* uo, float* xo, int* st,
+                                int* it, void* stream) {
+  const int rc = f110qp_solve_batch_ex_dev(c, batch, x0, ul, xr, hs, uo, xo, st, it, nullptr, nullptr, stream);
+  if (rc) return rc;
+  // busy wait: a single-tick solve is ~10 us, where the blocking wait's wake-up is a visible share
+  hipError_t e;
+  while ((e = hipStreamQuery((hipStream_t)stream)) == hipErrorNotReady) {
+  }
+  if (e != hipSuccess) return hip_fail(e, "hipStreamQuery");
+  return F110QP_OK;
+}
+
 int f110qp_solve_batch_ex_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                               const float* xr, const float* hs, float* uo, float* xo, int* st,
                               int* it, double* obj, double* cost, void* stream) {

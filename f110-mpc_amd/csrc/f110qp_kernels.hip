@@ -77,6 +77,7 @@ __global__ __launch_bounds__(256) void gap_screen_kernel(const int B, const int 
 // the launch (an atomic append in the lane kernel's wave completion order put them late; same-box
 // A/B on C3: step 236-242 -> 225 us with this order).
 constexpr int kPrioMax = 127;
+static_assert(kPrioMax + 1 == 128, "gap_order_kernel scans the priorities as two 64-lane rows");
 __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int* __restrict__ prio,
                                                          int* __restrict__ count, int* __restrict__ list,
                                                          int* __restrict__ zero) {
@@ -90,14 +91,28 @@ __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int*
     if (p > 0) atomicAdd(&hist[p], 1);
   }
   __syncthreads();
-  if (t == 0) {  // descending exclusive offsets: the highest priority first
-    int run = 0;
-    for (int p = kPrioMax; p >= 1; p--) {
-      off[p] = run;
-      run += hist[p];
+  // descending exclusive offsets (the highest priority first) by two 64-lane scans: thread
+  // t < 128 holds priority 127 - t (priority 0, not listed, contributes nothing)
+  __shared__ int wtot;
+  int inc = 0, own = 0;
+  if (t < kPrioMax + 1) {
+    own = (t < kPrioMax) ? hist[kPrioMax - t] : 0;
+    inc = own;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(inc, d, 64);
+      inc += ((t & 63) >= d) ? o : 0;
     }
-    *count = run;
-    if (zero) *zero = 0;  // the re-check count the GI kernel appends to next
+    if (t == 63) wtot = inc;
+  }
+  __syncthreads();
+  if (t < kPrioMax + 1) {
+    if (t >= 64) inc += wtot;
+    if (t < kPrioMax) off[kPrioMax - t] = inc - own;
+    if (t == kPrioMax) {
+      *count = inc;
+      if (zero) *zero = 0;  // the re-check count the GI kernel appends to next
+    }
   }
   __syncthreads();
   for (int b = t; b < B; b += 1024) {

@@ -63,6 +63,7 @@ EXPORTED = (
     "f110qp_destroy",
     "f110qp_solve_batch",
     "f110qp_solve_batch_dev",
+    "f110qp_solve_batch_dev_sync",
     "f110qp_solve_grouped",
     "f110qp_solve_grouped_dev",
     "f110qp_condense_debug_dev",
@@ -143,6 +144,7 @@ def load():
     L.f110qp_destroy.argtypes = [C.c_void_p]
     L.f110qp_solve_batch.argtypes = [C.c_void_p, C.c_int] + [fp] * 8
     L.f110qp_solve_batch_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 9
+    L.f110qp_solve_batch_dev_sync.argtypes = [C.c_void_p, C.c_int] + [fp] * 9
     L.f110qp_solve_grouped.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 4
     L.f110qp_solve_grouped_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 5 + [C.c_int] + [fp] * 5
     L.f110qp_solve_batch_ex.argtypes = [C.c_void_p, C.c_int] + [fp] * 10
@@ -349,16 +351,18 @@ class Solver:
                                                _tp(u_out), _tp(x_out), _tp(status), _tp(iters),
                                                C.c_void_p(stream.cuda_stream)), "f110qp_solve_batch_dev")
 
-    def prepare_dev(self, x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters=None, stream=None):
+    def prepare_dev(self, x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters=None, stream=None,
+                    sync=False):
         """A launcher for repeated f110qp_solve_batch_dev calls on the same device buffers: the
         ctypes arguments are converted once, each call is one C call (what a C++ caller of the ABI
-        pays; bench.py's timed steps use it so Python argument marshalling is not the step)."""
+        pays; bench.py's timed steps use it so Python argument marshalling is not the step).
+        sync=True: f110qp_solve_batch_dev_sync (returns with the results in device memory)."""
         import torch
 
         self._check_dev(x0, u_lin, x_ref, halfspace, u_out, x_out, status, iters)
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
-        fn = self.lib.f110qp_solve_batch_dev
+        fn = self.lib.f110qp_solve_batch_dev_sync if sync else self.lib.f110qp_solve_batch_dev
         args = (self._h, x0.shape[0], _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace), _tp(u_out), _tp(x_out),
                 _tp(status), _tp(iters), C.c_void_p(stream.cuda_stream))
 

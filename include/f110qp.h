@@ -175,6 +175,13 @@ int f110qp_solve_batch_dev(f110qp_ctx* ctx, int batch, const float* x0, const fl
                            const float* x_ref, const float* halfspace, float* u_out,
                            float* x_out, int* status, int* iters, void* stream);
 
+/* f110qp_solve_batch_dev, then a busy wait on `stream` until the results are in device memory:
+ * one call per control tick for a caller that needs the answer before it returns, as
+ * solver_.solve() + getSolution do in MPC::Update (src/mpc.cpp:133-142). */
+int f110qp_solve_batch_dev_sync(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
+                                const float* x_ref, const float* halfspace, float* u_out,
+                                float* x_out, int* status, int* iters, void* stream);
+
 /* Grouped solve: the candidates of one control tick share their linearisation point.
  * Model::Linearize depends only on (theta0, v, delta) (src/model.cpp:30-59), so the candidate
  * mini-paths of one pose (src/project.cpp:76-113) share A, B, C, the condensed Hessian H and

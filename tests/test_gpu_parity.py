@@ -932,3 +932,27 @@ def test_warm_traffic_switches_off_and_back_on(oracle, capi):
     warm.close()
     cold.close()
     assert its[-1] <= 1.01 and its[-1] < its[0], its
+
+
+def test_solve_batch_dev_sync_matches_async(capi):
+    """f110qp_solve_batch_dev_sync returns with the results in device memory, equal to the
+    asynchronous entry point's (one tick and a C2-size batch)."""
+    import torch
+    N = 20
+    for B in (1, 1024):
+        w = workload.make_batch(B, N, seed=90 + B)
+        d = {k: torch.from_numpy(np.ascontiguousarray(w[k])).cuda() for k in ("x0", "u_lin", "x_ref")}
+        s = capi.Solver(capi.default_config(N))
+        outs = []
+        for sync in (False, True):
+            uo = torch.empty((B, N, 2), dtype=torch.float32, device="cuda")
+            xo = torch.empty((B, N + 1, 3), dtype=torch.float32, device="cuda")
+            st = torch.empty((B,), dtype=torch.int32, device="cuda")
+            launch = s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], None, uo, xo, st, sync=sync)
+            launch()
+            if not sync:
+                torch.cuda.synchronize()
+            outs.append((uo.cpu().numpy(), xo.cpu().numpy(), st.cpu().numpy()))
+        s.close()
+        for a, b in zip(outs[0], outs[1]):
+            np.testing.assert_array_equal(a, b)
