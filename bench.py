@@ -251,7 +251,7 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
         if i >= 20:
             dev_t.append(time.perf_counter() - t0)
     # the same through the prepared launcher: one C call per tick that returns with the answer
-    # (f110qp_solve_batch_dev_sync: launch, then a busy wait on the stream; what a C++ caller of the
+    # (f110qp_solve_batch_dev_sync: launch, then hipStreamSynchronize; what a C++ caller of the
     # ABI pays), no ctypes argument conversion
     launch1s = s1.prepare_dev(one["x0"], one["u_lin"], one["x_ref"], h1, uo, xo, st, stream=stream, sync=True)
     for i in range(reps + 20):
@@ -298,7 +298,7 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
             "single_qp_kernel_us": k1_us,
             "single_qp_backend": ("lane" + (f" (S = {seg1})" if seg1 > 1 else "")) if be1 == capi.BACKEND_LANE else "wave",
             "note": "wall clock per call incl. launch + wait for the results: single_qp_device is one C call "
-                    "(f110qp_solve_batch_dev_sync: launch + busy wait on the stream), _async_then_sync the "
+                    "(f110qp_solve_batch_dev_sync: launch + hipStreamSynchronize), _async_then_sync the "
                     "asynchronous launcher then torch's stream synchronize, _ctypes with the per-call argument "
                     "conversion; host-pointer path adds H2D/D2H over PCIe"}
 

@@ -350,11 +350,9 @@ int f110qp_solve_batch_dev_sync(f110qp_ctx* c, int batch, const float* x0, const
                                 int* it, void* stream) {
   const int rc = f110qp_solve_batch_ex_dev(c, batch, x0, ul, xr, hs, uo, xo, st, it, nullptr, nullptr, stream);
   if (rc) return rc;
-  // busy wait: a single-tick solve is ~10 us, where the blocking wait's wake-up is a visible share
-  hipError_t e;
-  while ((e = hipStreamQuery((hipStream_t)stream)) == hipErrorNotReady) {
-  }
-  if (e != hipSuccess) return hip_fail(e, "hipStreamQuery");
+  // (a hipStreamQuery spin measured slower: B = 1 p50 22.9 against 20.8 us for the synchronize)
+  const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   return F110QP_OK;
 }
 

@@ -175,7 +175,7 @@ int f110qp_solve_batch_dev(f110qp_ctx* ctx, int batch, const float* x0, const fl
                            const float* x_ref, const float* halfspace, float* u_out,
                            float* x_out, int* status, int* iters, void* stream);
 
-/* f110qp_solve_batch_dev, then a busy wait on `stream` until the results are in device memory:
+/* f110qp_solve_batch_dev, then a wait on `stream` until the results are in device memory:
  * one call per control tick for a caller that needs the answer before it returns, as
  * solver_.solve() + getSolution do in MPC::Update (src/mpc.cpp:133-142). */
 int f110qp_solve_batch_dev_sync(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
