@@ -314,7 +314,7 @@ struct Smem {
   // gap rows only: V[slot][var] = W n_slot. With box rows alone V and S_A = N_A' W N_A are
   // signed entries of W (n_j = +-e_var) and are read from W directly.
   float V[GAP ? NUM : 1][NUM];
-  float vec[VN];                   // broadcast scratch (one entry per variable)
+  alignas(16) float vec[VN];       // broadcast scratch (one entry per variable)
   float vec2[VN];
   float stX[NST], stY[NST];        // per-stage linear rollout (stage 1..N)
   double rx[VN], ry[VN];           // recentred reference of the variable's stage (fp64: x_ref - x0
@@ -500,6 +500,9 @@ __device__ __forceinline__ void chol_delete(Smem<NUM, GAP>& sm, int lane, int q,
 
 // y = W x with x in sm.vec; W symmetric so the lane reads column v (consecutive addresses
 // across lanes, conflict free). Variables >= NUM get 0.
+#ifndef F110QP_MATVEC_SPLIT
+#define F110QP_MATVEC_SPLIT 1
+#endif
 template <int NUM, bool GAP, int R>
 __device__ __forceinline__ void matvec_W(Smem<NUM, GAP>& sm, int lane, float (&y)[R]) {
   int c[R];
@@ -509,12 +512,35 @@ __device__ __forceinline__ void matvec_W(Smem<NUM, GAP>& sm, int lane, float (&y
     c[r] = v < NUM ? v : NUM - 1;
     y[r] = 0.f;
   }
+#if F110QP_MATVEC_SPLIT
+  // x broadcast four entries per 16-B LDS read; four independent accumulator chains (the single
+  // chain was NUM dependent FMAs per call, one call per GI step)
+  static_assert(NUM % 4 == 0, "matvec_W reads x in float4");
+  float y1[R], y2[R], y3[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) { y1[r] = 0.f; y2[r] = 0.f; y3[r] = 0.f; }
+  const float4* x4 = reinterpret_cast<const float4*>(sm.vec);
+#pragma unroll
+  for (int j = 0; j < NUM; j += 4) {
+    const float4 xj = x4[j / 4];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      y[r] = fmaf(sm.W[j][c[r]], xj.x, y[r]);
+      y1[r] = fmaf(sm.W[j + 1][c[r]], xj.y, y1[r]);
+      y2[r] = fmaf(sm.W[j + 2][c[r]], xj.z, y2[r]);
+      y3[r] = fmaf(sm.W[j + 3][c[r]], xj.w, y3[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) y[r] = (y[r] + y1[r]) + (y2[r] + y3[r]);
+#else
 #pragma unroll
   for (int j = 0; j < NUM; j++) {
     const float xj = sm.vec[j];
 #pragma unroll
     for (int r = 0; r < R; r++) y[r] = fmaf(sm.W[j][c[r]], xj, y[r]);
   }
+#endif
 #pragma unroll
   for (int r = 0; r < R; r++) y[r] = (64 * r + lane < NUM) ? y[r] : 0.f;
 }
@@ -1106,6 +1132,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   STAMP(t_grad);
   // ---- 4. active set -----------------------------------------------------------------------
   float xv[R];           // GI iterate (fp32)
+  float xunc[R];         // GI's start, the unconstrained optimum -W g (the negative-multiplier re-entry)
   int actf[R];           // bit t set when constraint 3*v+t is active
   int slot_id[R];        // constraint id of active slot (64r + lane), -1 if none
   float mult[R];         // its multiplier
@@ -1427,7 +1454,10 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     // x = -W g  (g in sm.vec)
     matvec_W<NUM, GAP, R>(sm, lane, xv);
 #pragma unroll
-    for (int r = 0; r < R; r++) xv[r] = valid[r] ? -xv[r] : 0.f;
+    for (int r = 0; r < R; r++) {
+      xv[r] = valid[r] ? -xv[r] : 0.f;
+      xunc[r] = xv[r];
+    }
     wsync();
 #pragma unroll
     for (int r = 0; r < R; r++) actf[r] = 0;
@@ -1546,28 +1576,10 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
             r1[r] = valid[r] ? r1[r] - ml + mu : 0.0;
           }
         };
-        bool gi_ref_ok = false;
-        float prev = 3.0e38f;
-        for (int rs = 0; rs < kRefineMax; rs++) {
-          wsync();
-          double r1[R];
-          kkt_res(false, r1);
-#pragma unroll
-          for (int r = 0; r < R; r++) {
-            sm.d64[vv[r]] = u64[r];
-            if (GAP && a == 1 && kk[r] < N) { sm.sx64[kk[r] + 1] = px[r]; sm.sy64[kk[r] + 1] = py[r]; }
-            sm.vec[vv[r]] = (float)r1[r];
-          }
-          wsync();
-          // w1 = W r1 (the correction's first product) and the residual's W-norm r1'W r1
-          float w1[R];
-          matvec_W<NUM, GAP, R>(sm, lane, w1);
-          double rsq = 0.0;
-#pragma unroll
-          for (int r = 0; r < R; r++) rsq += valid[r] ? r1[r] * (double)w1[r] : 0.0;
-          rsq = wave_sum(rsq);
-          // r2_j = n_j'u - b_j on the active rows (fp64); active rows must hold with equality
-          float r2[R], r2n = 0.f;
+        // r2_j = n_j'u - b_j on the active rows (fp64, from sm.d64 / sx64 / sy64); active rows must
+        // hold with equality. Returns max |r2_j| / scale over the slots (wave-uniform).
+        auto act_res = [&](float (&r2)[R]) __attribute__((always_inline)) -> float {
+          float r2n = 0.f;
 #pragma unroll
           for (int r = 0; r < R; r++) {
             r2[r] = 0.f;
@@ -1592,12 +1604,33 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
               r2n = fmaxf(r2n, (float)(fabs(r2d) / sc));
             }
           }
-          {
-            int dummy = 0;
-            r2n = -r2n;
-            wave_argmin(r2n, dummy);
-            r2n = -r2n;
+          int dummy = 0;
+          r2n = -r2n;
+          wave_argmin(r2n, dummy);
+          return -r2n;
+        };
+        bool gi_ref_ok = false;
+        float prev = 3.0e38f;
+        for (int rs = 0; rs < kRefineMax; rs++) {
+          wsync();
+          double r1[R];
+          kkt_res(false, r1);
+#pragma unroll
+          for (int r = 0; r < R; r++) {
+            sm.d64[vv[r]] = u64[r];
+            if (GAP && a == 1 && kk[r] < N) { sm.sx64[kk[r] + 1] = px[r]; sm.sy64[kk[r] + 1] = py[r]; }
+            sm.vec[vv[r]] = (float)r1[r];
           }
+          wsync();
+          // w1 = W r1 (the correction's first product) and the residual's W-norm r1'W r1
+          float w1[R];
+          matvec_W<NUM, GAP, R>(sm, lane, w1);
+          double rsq = 0.0;
+#pragma unroll
+          for (int r = 0; r < R; r++) rsq += valid[r] ? r1[r] * (double)w1[r] : 0.0;
+          rsq = wave_sum(rsq);
+          float r2[R];
+          const float r2n = act_res(r2);
           if (rsq <= 0.25 * thr2 && r2n <= 1e-9f) { gi_ref_ok = true; break; }
           if (rs + 1 == kRefineMax) break;
           // v1_j = n_j' w1
@@ -1695,20 +1728,134 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           bool neg = false;
 #pragma unroll
           for (int r = 0; r < R; r++) neg = neg || (64 * r + lane < q && sm.cmult[slot_id[r]] < 0.0);
-          if (cert && __ballot(neg) != 0ull) {
+          // The residual bound itself, at the final u64 with the multipliers clamped at 0, when the
+          // refinement stopped short of its own test (stalled or at kRefineMax: the bound does not
+          // care how the point was reached) or a multiplier is negative
+          if (bid64 == 0x7fffffff && (!gi_ref_ok || __ballot(neg) != 0ull)) {
             double r1c[R];
+            wsync();
             kkt_res(true, r1c);
-            wsync();
 #pragma unroll
-            for (int r = 0; r < R; r++) sm.vec[vv[r]] = (float)r1c[r];
+            for (int r = 0; r < R; r++) {
+              sm.d64[vv[r]] = u64[r];
+              if (GAP && a == 1 && kk[r] < N) { sm.sx64[kk[r] + 1] = px[r]; sm.sy64[kk[r] + 1] = py[r]; }
+              sm.vec[vv[r]] = (float)r1c[r];
+            }
             wsync();
-            float wc[R];
+            float wc[R], r2c[R];
             matvec_W<NUM, GAP, R>(sm, lane, wc);
+            const float r2nc = act_res(r2c);
             double rsq = 0.0;
 #pragma unroll
             for (int r = 0; r < R; r++) rsq += valid[r] ? r1c[r] * (double)wc[r] : 0.0;
             rsq = wave_sum(rsq);
-            cert = rsq <= thr2;
+            cert = rsq <= thr2 && r2nc <= 1e-9f;
+          }
+          if constexpr (GAP) {
+            // Negative-multiplier re-entry: the refined set holds a row with a negative multiplier
+            // (fp32 GI kept a row it should have released; the clamped residual then fails the
+            // bound). Drop the most negative, re-solve the equality QP of the remaining set for its
+            // multipliers, S_A mu = -s_A(x_unc) (dropping again while one is negative), and continue
+            // GI from the dual-feasible x = x_unc + sum mu_j V_j, instead of sending the QP to the
+            // fp64 re-check (one heavy QP there costs ~170 us on the C3 launch).
+            if (!cert && bid64 == 0x7fffffff && reentries < 4 && __ballot(neg) != 0ull) {
+              float mneg = 0.f;
+              int kd = 0x7fffffff;
+#pragma unroll
+              for (int r = 0; r < R; r++) {
+                const int sl = 64 * r + lane;
+                if (sl < q) {
+                  const float m = (float)sm.cmult[slot_id[r]];
+                  if (m < mneg) { mneg = m; kd = sl; }
+                }
+              }
+              wave_argmin(mneg, kd);
+              // slacks of the rows at x_unc, by variable: box rows from x_unc itself, gap rows from
+              // its linear rollout
+              {
+                float X[R], Y[R];
+                rollout_lin_f32<R>(sm.M, lane, xunc, X, Y);
+                wsync();
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                  sm.vec[vv[r]] = (a ? ga1 : ga0) * X[r] + (a ? gb1 : gb0) * Y[r] + cgap[r];
+                  sm.vec2[vv[r]] = xunc[r];
+                }
+                wsync();
+              }
+              float mu[R];
+#pragma unroll
+              for (int r = 0; r < R; r++) mu[r] = mult[r];
+              while (kd != 0x7fffffff) {
+                const int did = rl_i<R>(slot_id, kd);
+                const int down = did / 3;
+#pragma unroll
+                for (int r = 0; r < R; r++)
+                  if (vv[r] == down) actf[r] &= ~(1 << (did - 3 * down));
+                int sid_n[R];
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                  sid_n[r] = __shfl_down(slot_id[r], 1, 64);
+                  if (r + 1 < R) {
+                    const int s_next = readlane_i(slot_id[r + 1 < R ? r + 1 : r], 0);
+                    if (lane == 63) sid_n[r] = s_next;
+                  }
+                }
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                  const int sl = 64 * r + lane;
+                  if (sl >= kd && sl < q - 1) slot_id[r] = sid_n[r];
+                  if (sl == q - 1) slot_id[r] = -1;
+                }
+#pragma unroll
+                for (int r = 0; r < R; r++)
+                  if (vv[r] < NUM)
+                    for (int j = kd; j < q - 1; j++) sm.V[j][vv[r]] = sm.V[j + 1][vv[r]];
+                chol_delete<NUM, GAP, R>(sm, lane, q, kd, rdiag);
+                q--;
+                wsync();
+                // multipliers of the equality QP on the remaining set
+                float rhs[R], lv[R];
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                  rhs[r] = 0.f;
+                  if (64 * r + lane < q) {
+                    const int owner = slot_id[r] / 3, t = slot_id[r] - 3 * owner;
+                    const float xo = sm.vec2[owner];
+                    const float sl = t == 0 ? xo - ((owner & 1) ? umin1 : umin0)
+                                   : (t == 1 ? ((owner & 1) ? umax1 : umax0) - xo : sm.vec[owner]);
+                    rhs[r] = -sl;
+                  }
+                }
+                tri_forward<NUM, GAP, R>(sm, lane, q, rdiag, rhs, lv);
+                tri_backward<NUM, GAP, R>(sm, lane, q, rdiag, lv, mu);
+                mneg = 0.f;
+                kd = 0x7fffffff;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                  const int sl = 64 * r + lane;
+                  if (sl < q && mu[r] < mneg) { mneg = mu[r]; kd = sl; }
+                }
+                wave_argmin(mneg, kd);
+                it++;
+              }
+#pragma unroll
+              for (int r = 0; r < R; r++) {
+                mult[r] = (64 * r + lane < q) ? mu[r] : 0.f;
+                xv[r] = xunc[r];
+              }
+              for (int j = 0; j < q; j++) {
+                const float mj = rl_f<R>(mu, j);
+#pragma unroll
+                for (int r = 0; r < R; r++) xv[r] = fmaf(mj, sm.V[j][cl[r]], xv[r]);
+              }
+#pragma unroll
+              for (int r = 0; r < R; r++) xv[r] = valid[r] ? xv[r] : 0.f;
+              reentries++;
+              forced_p = -1;
+              wsync();
+              continue;
+            }
           }
           inexact = !cert;
           final_ok = true;
@@ -1792,9 +1939,9 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       STAMP_ACC(acc_tri, t_c);
       STAMP(t_d);
       // z = w - sum_j r_j V[j]  (primal step direction)
-      float z[R];
+      float z[R], z2[R];  // two accumulator chains (even / odd slots of a block)
 #pragma unroll
-      for (int r = 0; r < R; r++) z[r] = w[r];
+      for (int r = 0; r < R; r++) { z[r] = w[r]; z2[r] = 0.f; }
       int j = 0;
       if constexpr (GAP) {  // V rows in blocks: the block's loads first (see tri_forward)
         for (; j + kTriBlock <= q; j += kTriBlock) {
@@ -1807,10 +1954,15 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           for (int jb = 0; jb < kTriBlock; jb++) {
             const float rj = rl_f<R>(rr, j + jb);
 #pragma unroll
-            for (int r = 0; r < R; r++) z[r] = fmaf(-rj, vb[jb][r], z[r]);
+            for (int r = 0; r < R; r++) {
+              if (jb & 1) z2[r] = fmaf(-rj, vb[jb][r], z2[r]);
+              else z[r] = fmaf(-rj, vb[jb][r], z[r]);
+            }
           }
         }
       }
+#pragma unroll
+      for (int r = 0; r < R; r++) z[r] += z2[r];
       for (; j < q; j++) {
         const float rj = rl_f<R>(rr, j);
         const int sj = GAP ? 0 : rl_i<R>(slot_id, j);

@@ -85,6 +85,19 @@ def test_c3_full_batch_gap_rows(oracle, capi):
     assert (st == capi.SOLVED).mean() > 0.99
 
 
+def test_c3_bench_batch_gap_rows(oracle, capi):
+    """The bench's own C3 batch (bench.py seeds: make_batch 1000, make_scans 2000): every QP exact
+    against the oracle. QP 3008 of it took GI's negative-multiplier re-entry when that was added
+    (solve_kernel.h: the refined set held a row with a negative multiplier; the row is dropped and
+    GI continues instead of the fp64 re-check)."""
+    B = 4096
+    w = workload.make_batch(B, 20, seed=1000)
+    ranges, *geom = workload.make_scans(B, seed=2000)
+    hs = halfspaces_oracle(oracle, w["x0"], ranges, geom)
+    u, x, st, it = check(oracle, capi, 20, w, hs, gap=True)
+    assert (st == capi.SOLVED).all()
+
+
 @pytest.mark.parametrize("N", [1, 2, 3, 7, 10, 16, 17, 24, 25, 30, 32, 33, 36, 40, 41, 47, 48])
 def test_horizons(oracle, capi, N):
     w = workload.make_batch(200, N, seed=300 + N, lateral=0.6)
