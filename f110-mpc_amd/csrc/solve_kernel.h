@@ -309,7 +309,9 @@ struct Smem {
   static constexpr int R = (NUM + 63) / 64;
   static constexpr int VN = 64 * R;      // per-variable vectors (one entry per lane and row)
   static constexpr int NST = NUM / 2 + 1;  // stages 0..N
-  alignas(16) float W[NUM][NUM];   // W = H^-1, row-major (symmetric: row p == column p)
+  // W = H^-1, row-major (symmetric: row p == column p). Rows padded to NUM + 4: matvec_W reads a
+  // lane's own row as float4, and a stride of NUM + 4 words puts 16 such lanes on distinct banks
+  alignas(16) float W[NUM][NUM + 4];
   float L[NUM][NUM + 1];           // Cholesky factor of S_A (lower), slots x slots
   // gap rows only: V[slot][var] = W n_slot. With box rows alone V and S_A = N_A' W N_A are
   // signed entries of W (n_j = +-e_var) and are read from W directly.
@@ -513,22 +515,28 @@ __device__ __forceinline__ void matvec_W(Smem<NUM, GAP>& sm, int lane, float (&y
     y[r] = 0.f;
   }
 #if F110QP_MATVEC_SPLIT
-  // x broadcast four entries per 16-B LDS read; four independent accumulator chains (the single
-  // chain was NUM dependent FMAs per call, one call per GI step)
-  static_assert(NUM % 4 == 0, "matvec_W reads x in float4");
+  // y_c = sum_j W[c][j] x_j over the lane's own row (W symmetric): four entries of the row and of
+  // the broadcast x per 16-B LDS read, four independent accumulator chains (the column form was
+  // NUM dependent FMAs and 2 NUM LDS reads per call, one call per GI step)
+  static_assert(NUM % 4 == 0, "matvec_W reads in float4");
   float y1[R], y2[R], y3[R];
+  const float4* wr[R];
 #pragma unroll
-  for (int r = 0; r < R; r++) { y1[r] = 0.f; y2[r] = 0.f; y3[r] = 0.f; }
+  for (int r = 0; r < R; r++) {
+    y1[r] = 0.f; y2[r] = 0.f; y3[r] = 0.f;
+    wr[r] = reinterpret_cast<const float4*>(sm.W[c[r]]);
+  }
   const float4* x4 = reinterpret_cast<const float4*>(sm.vec);
 #pragma unroll
-  for (int j = 0; j < NUM; j += 4) {
-    const float4 xj = x4[j / 4];
+  for (int j = 0; j < NUM / 4; j++) {
+    const float4 xj = x4[j];
 #pragma unroll
     for (int r = 0; r < R; r++) {
-      y[r] = fmaf(sm.W[j][c[r]], xj.x, y[r]);
-      y1[r] = fmaf(sm.W[j + 1][c[r]], xj.y, y1[r]);
-      y2[r] = fmaf(sm.W[j + 2][c[r]], xj.z, y2[r]);
-      y3[r] = fmaf(sm.W[j + 3][c[r]], xj.w, y3[r]);
+      const float4 wv = wr[r][j];
+      y[r] = fmaf(wv.x, xj.x, y[r]);
+      y1[r] = fmaf(wv.y, xj.y, y1[r]);
+      y2[r] = fmaf(wv.z, xj.z, y2[r]);
+      y3[r] = fmaf(wv.w, xj.w, y3[r]);
     }
   }
 #pragma unroll
