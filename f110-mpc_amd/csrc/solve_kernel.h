@@ -801,6 +801,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     lb[r] = valid[r] ? (a ? umin1 : umin0) : -3.0e38f;
     ub[r] = valid[r] ? (a ? umax1 : umax0) : 3.0e38f;
   }
+  const float il0 = 1.f / (1.f + fabsf(umin0)), il1 = 1.f / (1.f + fabsf(umin1));
+  const float iu0 = 1.f / (1.f + fabsf(umax0)), iu1 = 1.f / (1.f + fabsf(umax1));
 
   // gap rows: a*x + b*y >= -(c+0.5) (constraints.cpp:255-264, mpc.cpp:297-298), recentred
   float ga0 = 0.f, ga1 = 0.f, gb0 = 0.f, gb1 = 0.f;
@@ -1497,7 +1499,9 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         if (!valid[r]) continue;
         const int v = vv[r];
         const float s0 = xv[r] - lb[r], s1 = ub[r] - xv[r];
-        const float v0 = s0 / (1.f + fabsf(lb[r])), v1 = s1 / (1.f + fabsf(ub[r]));
+        // scaled slacks s / (1 + |bound|); the bound of a variable is its input's, so the two
+        // scales are wave-uniform per lane parity (a reciprocal multiply, no fp32 division)
+        const float v0 = s0 * (a ? il1 : il0), v1 = s1 * (a ? iu1 : iu0);
         if (!(actf[r] & 1) && v0 < -1e-6f && v0 < best) { best = v0; bid = 3 * v; sraw = s0; }
         if (!(actf[r] & 2) && v1 < -1e-6f && v1 < best) { best = v1; bid = 3 * v + 1; sraw = s1; }
         if (GAP) {
