@@ -2176,9 +2176,8 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
     unsigned long long* o = g_stamps + (size_t)b * kStampSlots;
     o[0] = t_lin - t_start; o[1] = t_grad - t_inv; o[2] = t_hess - t_lin; o[3] = t_inv - t_hess;
     o[4] = t_gi - t_grad - acc_refine; o[5] = acc_refine; o[6] = t_end - t_gi; o[7] = t_end - t_start;
-    o[8] = acc_s1; o[9] = acc_pdas; o[10] = acc_vj; o[11] = acc_tri; o[12] = acc_z; o[13] = acc_step;
+    o[8] = acc_s1; o[9] = acc_pdas + acc_w; o[10] = acc_vj; o[11] = acc_tri; o[12] = acc_z; o[13] = acc_step;
     o[14] = acc_upd; o[15] = it;
-    (void)acc_w;
   }
 #endif
 }

@@ -28,7 +28,7 @@ buf = np.zeros((B, 16), np.uint64)
 L.f110qp_read_stamps.argtypes = [C.c_void_p, C.c_int]
 L.f110qp_read_stamps(C.c_void_p(buf.ctypes.data), B)
 names = ["inputs+linearize", "gradient g (fp64 scans)", "hessian (closed form)", "sweep inverse", "active set (fp32)",
-         "refinement+fp64 check", "outputs", "total", " gi: step1 search", " pdas warm start (box)", " gi: v_j gather",
+         "refinement+fp64 check", "outputs", "total", " gi: step1 search", " pdas (box) | gi: W n_p", " gi: v_j gather",
          " gi: tri solves", " gi: z update", " gi: step lengths", " gi: append slot"]
 tot = buf[:, 7].astype(float)
 print(f"B={B} N={N} gap={gap} iters mean {it.mean():.2f} max {it.max()}")
@@ -43,3 +43,4 @@ q = np.percentile(tot, [50, 90, 99, 100])
 imax = int(np.argmax(tot))
 print(f"total cycles p50 {q[0]:.0f} p90 {q[1]:.0f} p99 {q[2]:.0f} max {q[3]:.0f} (slowest QP: {int(it_[imax])} iterations, "
       f"gi {buf[imax, 4]:.0f}, refine {buf[imax, 5]:.0f}); iteration histogram {np.bincount(it_.astype(int), minlength=8)[:64].tolist()}")
+print("slowest QP by phase:", {n.strip(): int(buf[imax, i]) for i, n in enumerate(names)})
