@@ -315,7 +315,7 @@ struct Smem {
   float L[NUM][NUM + 1];           // Cholesky factor of S_A (lower), slots x slots
   // gap rows only: V[slot][var] = W n_slot. With box rows alone V and S_A = N_A' W N_A are
   // signed entries of W (n_j = +-e_var) and are read from W directly.
-  float V[GAP ? NUM : 1][NUM];
+  alignas(16) float V[GAP ? NUM : 1][NUM + 4];  // rows padded as W's (row reads in float4)
   alignas(16) float vec[VN];       // broadcast scratch (one entry per variable)
   float vec2[VN];
   float stX[NST], stY[NST];        // per-stage linear rollout (stage 1..N)
@@ -1921,23 +1921,45 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       }
       STAMP_ACC(acc_w, t_a);
       STAMP(t_b);
-      // v_j = n_j' w for the active slots
+      // v_j = n_j' W n_p for the active slots
+      float vj[R];
+      if constexpr (GAP) {
+        // = V_j' n_p (W symmetric, V_j = W n_j stored at slot j's add): a box candidate reads one
+        // entry of each V row, a gap candidate dots the slot's row with n_p, still in sm.vec from
+        // the W product; no rollout of w, no LDS round trip through stX / stY and no barrier
+        if (pt < 2) {
+          const float sg = (pt == 0) ? 1.f : -1.f;
 #pragma unroll
-      for (int r = 0; r < R; r++) sm.vec2[vv[r]] = w[r];
-      if (GAP) {
-        float Xw[R], Yw[R], wv[R];
+          for (int r = 0; r < R; r++) {
+            const int sl = 64 * r + lane;
+            vj[r] = (sl < q) ? sg * sm.V[sl < NUM ? sl : NUM - 1][pown] : 0.f;
+          }
+        } else {
+          const float4* x4 = reinterpret_cast<const float4*>(sm.vec);
 #pragma unroll
-        for (int r = 0; r < R; r++) wv[r] = valid[r] ? w[r] : 0.f;
-        rollout_lin_f32<R>(sm.M, lane, wv, Xw, Yw);
+          for (int r = 0; r < R; r++) {
+            const int sl = 64 * r + lane;
+            const float4* v4 = reinterpret_cast<const float4*>(sm.V[sl < NUM ? sl : NUM - 1]);
+            float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+#pragma unroll
+            for (int j4 = 0; j4 < NUM / 4; j4++) {
+              const float4 xv4 = x4[j4], vv4 = v4[j4];
+              d0 = fmaf(vv4.x, xv4.x, d0);
+              d1 = fmaf(vv4.y, xv4.y, d1);
+              d2 = fmaf(vv4.z, xv4.z, d2);
+              d3 = fmaf(vv4.w, xv4.w, d3);
+            }
+            vj[r] = (sl < q) ? (d0 + d1) + (d2 + d3) : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) sm.vec2[vv[r]] = w[r];
+        wsync();
 #pragma unroll
         for (int r = 0; r < R; r++)
-          if (a == 1 && kk[r] < N) { sm.stX[kk[r] + 1] = Xw[r]; sm.stY[kk[r] + 1] = Yw[r]; }
+          vj[r] = (64 * r + lane < q) ? slot_dot<NUM, GAP>(sm, slot_id[r], ga0, ga1, gb0, gb1) : 0.f;
       }
-      wsync();
-      float vj[R];
-#pragma unroll
-      for (int r = 0; r < R; r++)
-        vj[r] = (64 * r + lane < q) ? slot_dot<NUM, GAP>(sm, slot_id[r], ga0, ga1, gb0, gb1) : 0.f;
       STAMP_ACC(acc_vj, t_b);
       STAMP(t_c);
       // l = L^-1 v ; r = L^-T l  (r = S_A^-1 N_A' W n_p : dual step direction)
