@@ -1645,23 +1645,34 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           const float r2n = act_res(r2);
           if (rsq <= 0.25 * thr2 && r2n <= 1e-9f) { gi_ref_ok = true; break; }
           if (rs + 1 == kRefineMax) break;
-          // v1_j = n_j' w1
+          // v1_j = n_j' w1 (= V_j' r1 with the gap rows' stored V_j = W n_j: r1 is still in sm.vec
+          // from the W product, so no rollout of w1 and no barrier)
+          float rhs[R], lv[R], du[R];
+          if constexpr (GAP) {
+            const float4* x4 = reinterpret_cast<const float4*>(sm.vec);
 #pragma unroll
-          for (int r = 0; r < R; r++) sm.vec2[vv[r]] = w1[r];
-          if (GAP) {
-            float X1[R], Y1[R], w1v[R];
+            for (int r = 0; r < R; r++) {
+              const int sl = 64 * r + lane;
+              const float4* v4 = reinterpret_cast<const float4*>(sm.V[sl < NUM ? sl : NUM - 1]);
+              float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
 #pragma unroll
-            for (int r = 0; r < R; r++) w1v[r] = valid[r] ? w1[r] : 0.f;
-            rollout_lin_f32<R>(M, lane, w1v, X1, Y1);
+              for (int j4 = 0; j4 < NUM / 4; j4++) {
+                const float4 xr4 = x4[j4], vr4 = v4[j4];
+                d0 = fmaf(vr4.x, xr4.x, d0);
+                d1 = fmaf(vr4.y, xr4.y, d1);
+                d2 = fmaf(vr4.z, xr4.z, d2);
+                d3 = fmaf(vr4.w, xr4.w, d3);
+              }
+              rhs[r] = (sl < q) ? ((d0 + d1) + (d2 + d3)) - r2[r] : 0.f;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < R; r++) sm.vec2[vv[r]] = w1[r];
+            wsync();
 #pragma unroll
             for (int r = 0; r < R; r++)
-              if (a == 1 && kk[r] < N) { sm.stX[kk[r] + 1] = X1[r]; sm.stY[kk[r] + 1] = Y1[r]; }
+              rhs[r] = (64 * r + lane < q) ? slot_dot<NUM, GAP>(sm, slot_id[r], ga0, ga1, gb0, gb1) - r2[r] : 0.f;
           }
-          wsync();
-          float rhs[R], lv[R], du[R];
-#pragma unroll
-          for (int r = 0; r < R; r++)
-            rhs[r] = (64 * r + lane < q) ? slot_dot<NUM, GAP>(sm, slot_id[r], ga0, ga1, gb0, gb1) - r2[r] : 0.f;
           // du = S^-1 rhs ; dx = -w1 + sum_j du_j V[j]
           tri_forward<NUM, GAP, R>(sm, lane, q, rdiag, rhs, lv);
           tri_backward<NUM, GAP, R>(sm, lane, q, rdiag, lv, du);
