@@ -2024,7 +2024,9 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       for (int r = 0; r < R; r++) {
         const int s = 64 * r + lane;
         if (s < q && rr[r] > 0.f) {
-          const float tr = mult[r] / rr[r];
+          // (v_rcp: the ratio only ranks the blocking slot and sets the partial step, whose point
+          // the fp64 refinement corrects; an IEEE division is ~10 dependent instructions)
+          const float tr = mult[r] * __builtin_amdgcn_rcpf(rr[r]);
           if (tr < t1) { t1 = tr; k1 = s; }
         }
       }
