@@ -484,7 +484,8 @@ __device__ __forceinline__ void chol_delete(Smem<NUM, GAP>& sm, int lane, int q,
     }
     const float a = rl_f<R>(carry, j), b = rl_f<R>(y, j);
     const float h = sqrtf(a * a + b * b);
-    const float cs = a / h, sn = b / h;
+    const float ih = 1.f / h;  // one division per rotation (cs, sn and the new 1 / L[j][j])
+    const float cs = a * ih, sn = b * ih;
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const int row = 64 * r + lane;
@@ -494,7 +495,7 @@ __device__ __forceinline__ void chol_delete(Smem<NUM, GAP>& sm, int lane, int q,
       }
       if (row == j) {
         sm.L[row][j] = h;
-        rd[r] = 1.f / h;
+        rd[r] = ih;
       }
     }
   }
