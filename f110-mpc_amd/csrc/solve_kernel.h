@@ -234,13 +234,29 @@ __device__ __forceinline__ void rollout_f64(const Lin& M, int lane, const double
   }
 }
 
+// The linearisation's coefficients the fp32 GI uses, converted once and held in scalar registers
+// (the GI loop read the fp64 Lin from LDS and converted it on every rollout and normal)
+struct LinF {
+  float a02, a12, b00, b10, b20, b21;
+};
+__device__ __forceinline__ float sgpr_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ LinF lin_f32(const Lin& M) {
+  LinF f;
+  f.a02 = sgpr_f((float)M.a02); f.a12 = sgpr_f((float)M.a12);
+  f.b00 = sgpr_f((float)M.b00); f.b10 = sgpr_f((float)M.b10);
+  f.b20 = sgpr_f((float)M.b20); f.b21 = sgpr_f((float)M.b21);
+  return f;
+}
+
 // Linear part of the rollout (Gamma w, zero initial state, no affine term), fp32.
 template <int R>
-__device__ __forceinline__ void rollout_lin_f32(const Lin& M, int lane, const float (&w)[R],
+__device__ __forceinline__ void rollout_lin_f32(const LinF& M, int lane, const float (&w)[R],
                                                 float (&X)[R], float (&Y)[R]) {
   const int a = lane & 1;
-  const float beta = a ? (float)M.b21 : (float)M.b20;
-  const float a02 = (float)M.a02, a12 = (float)M.a12, b00 = (float)M.b00, b10 = (float)M.b10;
+  const float beta = a ? M.b21 : M.b20;
+  const float a02 = M.a02, a12 = M.a12, b00 = M.b00, b10 = M.b10;
   float s1[R], s2[R], s3[R];
 #pragma unroll
   for (int r = 0; r < R; r++) {
@@ -260,6 +276,13 @@ __device__ __forceinline__ void rollout_lin_f32(const Lin& M, int lane, const fl
     X[r] = a02 * sth + b00 * V;
     Y[r] = a12 * sth + b10 * V;
   }
+}
+
+template <int R>
+__device__ __forceinline__ void rollout_lin_f32(const Lin& M, int lane, const float (&w)[R],
+                                                float (&X)[R], float (&Y)[R]) {
+  const LinF f = {(float)M.a02, (float)M.a12, (float)M.b00, (float)M.b10, (float)M.b20, (float)M.b21};
+  rollout_lin_f32<R>(f, lane, w, X, Y);
 }
 
 // Gradient of the tracking objective (mpc.cpp:208-229 cost) minus the gap-row multiplier
@@ -1475,6 +1498,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
   }
 
   const bool gi_fallback = !final_ok && status == F110QP_SOLVED_ID;  // box rows: behind the fp64 PDAS
+  const LinF MF = lin_f32(sm.M);  // fp32 coefficients for GI's rollouts and normals
   // ---- 4b. dual active set (Goldfarb-Idnani, range space) ---------------------------------
   while (status == F110QP_SOLVED_ID && !final_ok) {
     // ---- step 1: most violated inactive constraint (fp32, scaled) ----
@@ -1487,7 +1511,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       forced_p = -1;
     } else {
       float X[R], Y[R];
-      if (GAP) rollout_lin_f32<R>(sm.M, lane, xv, X, Y);
+      if (GAP) rollout_lin_f32<R>(MF, lane, xv, X, Y);
       // Gap rows first (P.gap_first): a violated gap row enters before any box row; numpy model of
       // the GI loop on the C3 batch (tests/diag_gi_selection_model.py rules): max 34 -> 30
       // iterations, p99 17 either way. Otherwise one ranking over all rows.
@@ -1798,7 +1822,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
               // its linear rollout
               {
                 float X[R], Y[R];
-                rollout_lin_f32<R>(sm.M, lane, xunc, X, Y);
+                rollout_lin_f32<R>(MF, lane, xunc, X, Y);
                 wsync();
 #pragma unroll
                 for (int r = 0; r < R; r++) {
@@ -1911,16 +1935,14 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
       } else {
         const int ip = (pown >> 1) + 1, h = pown & 1;
         const float ah = h ? ga1 : ga0, bh = h ? gb1 : gb0;
-        const Lin& M = sm.M;
         float np[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
           np[r] = 0.f;
           if (valid[r] && kk[r] < ip) {
             const float d = (float)(ip - 1 - kk[r]);
-            const float fa02 = (float)M.a02, fa12 = (float)M.a12;
-            if (a == 0) np[r] = ah * ((float)M.b00 + fa02 * (float)M.b20 * d) + bh * ((float)M.b10 + fa12 * (float)M.b20 * d);
-            else np[r] = (ah * fa02 + bh * fa12) * (float)M.b21 * d;
+            if (a == 0) np[r] = ah * (MF.b00 + MF.a02 * MF.b20 * d) + bh * (MF.b10 + MF.a12 * MF.b20 * d);
+            else np[r] = (ah * MF.a02 + bh * MF.a12) * MF.b21 * d;
           }
           sm.vec[vv[r]] = np[r];
         }
