@@ -546,6 +546,8 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    if warm:
+        solver.warm_hits()  # zero the warm-start counters: the timed steps' own are read below
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -556,6 +558,16 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # what the warm start did in the timed steps (f110qp_warm_hits: device counters of the lane back
+    # ends; the wave back end reports none)
+    warm_eff = None
+    if warm:
+        wt_calls, wt_hits = solver.warm_hits()
+        warm_eff = {"calls_moving_warm_state": wt_calls, "calls": args.steps, "qps_seeded": wt_hits,
+                    "hit_rate": wt_hits / float(Bper * args.steps),
+                    "note": "counted on the device; a QP is seeded when its slot key (theta0, v, steer bits) "
+                            "repeats; the closed loop's theta0 moves every tick, so its solves are cold solves"
+                            if be_name == "lane" else "wave back end: not counted"}
     if world > 1:
         el = allreduce(el, dist.ReduceOp.MAX)
 
@@ -681,6 +693,7 @@ def main():
             **({"warm_key_hit_rate": key_hit,
                 "stream": "closed loop" if args.config != "c5_straight" else "straight (best case)"}
                if stream_cfg else {}),
+            **({"warm_effective": warm_eff} if warm_eff is not None else {}),
         },
         "roofline": {
             "bound": "hbm",

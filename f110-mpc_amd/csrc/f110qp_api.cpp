@@ -94,7 +94,9 @@ struct f110qp_ctx {
   DevBuf din, dout;   // their device copies for batches above kZeroCopyMaxBatch
   DevBuf wW, wkey, wact;  // warm-start slot state (config.warm_start)
   int warm_batch = 0;     // batch size the warm state was laid out for
-  int warm_calls = 0;     // warm calls since the state was laid out (WarmState::call)
+  unsigned warm_calls = 0;  // warm calls since the state was laid out (WarmState::call, wraps)
+  unsigned warm_prev[2] = {0u, 0u};  // the counters at the last f110qp_warm_hits
+  hipStream_t warm_stream = nullptr;  // stream of the last warm call
   DevBuf gW, gkey, glead;    // grouped mode: W = H^-1, key and leader per group
   DevBuf dgrp;               // host-pointer grouped calls: device copy of the group ids
   DevBuf lscr;               // lane back end: HBM Riccati scratch (when not in LDS)
@@ -107,8 +109,56 @@ struct f110qp_ctx {
   int lane_seg = 0;          // lane horizon segments per QP (LaneWork::seg: 0 auto, 1 off, 2/4/8)
   int lane_seg32 = 0;        // segmented kernel: force fp32 references + scratch (LaneWork::seg32)
   int gap_screen = -1;      // gap rows, AUTO: box screen on the lane kernel (-1 by batch, 0 off, 1 on)
+  int recheck_all = 0;      // gap rows: every QP of a call through the fp64 re-check alone (test build)
   hipStream_t stream = nullptr;
+  hipStream_t last_gap_stream = nullptr;  // stream of the last gap-row call (f110qp_last_recheck_count)
+  int last_gap_batch = 0;                 // its batch (0: no gap-row call yet)
 };
+
+#ifdef F110QP_TEST_HOOKS
+// Test / measurement build only (lib_test/libf110qp.so, -DF110QP_TEST_HOOKS): create-time knobs read
+// from the environment that force one kernel variant or rule of the dispatch, so the tests reach every
+// code path AUTO does not pick at their sizes. The product library (lib/libf110qp.so) reads no
+// environment variable: its behaviour is the config alone (the reference's solver settings are fixed
+// in code, src/mpc.cpp:98-99).
+static int env_int(const char* name, int lo, int hi, int* out) {
+  const char* e = std::getenv(name);
+  if (!e) return 0;
+  const int v = std::atoi(e);
+  if (v < lo || v > hi) return 0;
+  *out = v;
+  return 1;
+}
+
+static void test_hooks(f110qp_ctx* c) {
+  // PDAS passes of the lane back end before single least-index flips (0: single flips from pass 1)
+  env_int("F110QP_LANE_KMAX", 0, 64, &c->lane_kmax);
+  // QPs per wave of the lane back end (power of two <= 64)
+  int v;
+  if (env_int("F110QP_LANE_QPW", 1, 64, &v) && (v & (v - 1)) == 0) c->lane_qpw = v;
+  // lane scratch: 1 LDS fp64, 2 LDS fp32, 3 HBM fp64, 4 HBM fp32
+  env_int("F110QP_LANE_MODE", 0, 4, &c->lane_mode);
+  // 0: general-frame lane kernel even when q0 == q1
+  if (env_int("F110QP_LANE_ROT", 0, 1, &v)) c->lane_rot = v;
+  // 0: float references in LDS (no fp64 DREF array)
+  if (env_int("F110QP_LANE_DREF", 0, 1, &v)) c->lane_dref = v;
+  // horizon segments per QP (0 auto, 1 off, 2 / 4 / 8 forced where the horizon and the LDS allow)
+  if (env_int("F110QP_LANE_SEG", 0, 8, &v) && (v == 0 || v == 1 || v == 2 || v == 4 || v == 8)) c->lane_seg = v;
+  // 1: the segmented kernel's float references and scratch
+  if (env_int("F110QP_LANE_SEG_F32", 0, 1, &v)) c->lane_seg32 = v;
+  // gap rows: the box screen on (1) / off (0) at every batch size
+  if (env_int("F110QP_GAP_SCREEN", 0, 1, &v)) c->gap_screen = v;
+  // wave GI: 0 picks gap and box candidates by one ranking
+  if (env_int("F110QP_GI_GAPFIRST", 0, 1, &v)) c->kp.gap_first = v;
+  // lane kernels: PDAS passes per launch (measurement of the pass distribution: MAX_ITER past it)
+  env_int("F110QP_LANE_PASSCAP", 1, 999, &c->kp.pass_cap);
+  // wave kernel's box PDAS passes (0: GI from the unconstrained point)
+  env_int("F110QP_PDAS_MAX", 0, 64, &c->kp.pdas_max);
+  // gap rows: every QP of a call through the fp64 re-check (gi64_kernel.h) alone, no screen and no
+  // fp32 GI: the re-check's own answers, for its parity tests
+  if (env_int("F110QP_RECHECK_ALL", 0, 1, &v)) c->recheck_all = v;
+}
+#endif
 
 extern "C" {
 
@@ -146,13 +196,13 @@ static int validate_config(const f110qp_config* c) {
     if (!(c->u_min[i] <= c->u_max[i])) return fail(F110QP_ERR_INVALID, "u_min > u_max");
   }
   if (c->gap_mode != F110QP_GAP_INACTIVE && c->gap_mode != F110QP_GAP_ACTIVE)
-    return fail(F110QP_ERR_INVALID, "gap_mode must be F110QP_GAP_INACTIVE or F110QP_GAP_ACTIVE");
+    return fail(F110QP_ERR_INVALID, "gap_mode must be 0 (gap rows inactive) or 1 (active)");
   if (c->max_iter < 0) return fail(F110QP_ERR_INVALID, "max_iter must be >= 0");
   if (c->warm_start != 0 && c->warm_start != 1) return fail(F110QP_ERR_INVALID, "warm_start must be 0 or 1");
   if (c->x_ref_points != 0 && c->x_ref_points < c->horizon)
     return fail(F110QP_ERR_INVALID, "x_ref_points must be 0 (= horizon) or >= horizon");
   if (c->backend < F110QP_BACKEND_AUTO || c->backend > F110QP_BACKEND_LANE)
-    return fail(F110QP_ERR_INVALID, "backend must be F110QP_BACKEND_AUTO, _WAVE or _LANE");
+    return fail(F110QP_ERR_INVALID, "backend must be 0 (auto), 1 (wave) or 2 (lane)");
   return F110QP_OK;
 }
 
@@ -174,46 +224,10 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
     k.umin[i] = cfg->u_min[i];
     k.umax[i] = cfg->u_max[i];
   }
-  // test hook: F110QP_LANE_KMAX = PDAS passes of the lane back end before it switches to single
-  // least-index flips (0: single flips from the first pass)
-  if (const char* ek = std::getenv("F110QP_LANE_KMAX")) {
-    const int v = std::atoi(ek);
-    if (v >= 0 && v <= 64) c->lane_kmax = v;
-  }
-  // bench hook: F110QP_LANE_QPW = QPs per wave of the lane back end (power of two <= 64)
-  if (const char* eq = std::getenv("F110QP_LANE_QPW")) {
-    const int v = std::atoi(eq);
-    if (v >= 1 && v <= 64 && (v & (v - 1)) == 0) c->lane_qpw = v;
-  }
-  // test/bench hook: F110QP_LANE_MODE = 1 LDS fp64, 2 LDS fp32, 3 HBM fp64, 4 HBM fp32 scratch
-  if (const char* em = std::getenv("F110QP_LANE_MODE")) {
-    const int v = std::atoi(em);
-    if (v >= 0 && v <= 4) c->lane_mode = v;
-  }
-  // test hook: F110QP_LANE_ROT=0 forces the lane back end's general-frame kernel
-  if (const char* er = std::getenv("F110QP_LANE_ROT")) c->lane_rot = std::atoi(er) != 0;
-  // test hook: F110QP_LANE_DREF=0 keeps the lane back end's references as floats in LDS
-  if (const char* ed = std::getenv("F110QP_LANE_DREF")) c->lane_dref = std::atoi(ed) != 0;
-  // test/bench hook: F110QP_LANE_SEG = horizon segments per QP of the lane back end (0 auto,
-  // 1 off: lane_kernel.h only, 2 / 4 / 8 forced where the horizon and the LDS allow)
-  if (const char* es = std::getenv("F110QP_LANE_SEG")) {
-    const int v = std::atoi(es);
-    if (v == 0 || v == 1 || v == 2 || v == 4 || v == 8) c->lane_seg = v;
-  }
-  // test hook: F110QP_LANE_SEG_F32=1 forces the segmented kernel's float references and scratch
-  if (const char* ef = std::getenv("F110QP_LANE_SEG_F32")) c->lane_seg32 = std::atoi(ef) != 0;
-  if (const char* eg = std::getenv("F110QP_GAP_SCREEN")) c->gap_screen = std::atoi(eg) != 0;
-  if (const char* eg = std::getenv("F110QP_GI_GAPFIRST")) c->kp.gap_first = std::atoi(eg) != 0;
-  if (const char* ep = std::getenv("F110QP_LANE_PASSCAP")) {  // measurement: passes per lane launch
-    const int v = std::atoi(ep);
-    if (v > 0 && v < 1000) c->kp.pass_cap = v;
-  }
-  // test hook: F110QP_PDAS_MAX caps the wave kernel's box PDAS passes (0 = GI from scratch)
   k.pdas_max = 10;
-  if (const char* ep = std::getenv("F110QP_PDAS_MAX")) {
-    const int v = std::atoi(ep);
-    if (v >= 0 && v <= 64) k.pdas_max = v;
-  }
+#ifdef F110QP_TEST_HOOKS
+  test_hooks(c);
+#endif
   const int nu = 2 * cfg->horizon;
   k.max_iter = cfg->max_iter > 0 ? cfg->max_iter : 8 * (nu + (cfg->gap_mode ? nu : 0)) + 16;
   k.xr_stride = cfg->x_ref_points > 0 ? cfg->x_ref_points : cfg->horizon;
@@ -254,7 +268,8 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
   const size_t B = (size_t)batch, nu = 2 * (size_t)c->cfg.horizon;
   const size_t rows = (nu + 63) / 64;  // register rows per lane (act masks: 2 x 64 bits per row)
   hipError_t e;
-  // keys (16 B per QP), then the lane back ends' last-hit call (warm_traffic)
+  // keys (16 B per QP), then the lane back ends' last-hit call (warm_traffic) and the cumulative
+  // traffic-call and hit counters (f110qp_warm_hits)
   if ((e = c->wW.ensure(B * nu * nu * 4)) || (e = c->wkey.ensure(B * 16 + 16)) ||
       (e = c->wact.ensure(B * 16 * rows)))
     return hip_fail(e, "hipMalloc warm-start state");
@@ -263,12 +278,15 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
       return hip_fail(e, "hipMemsetAsync warm-start state");
     c->warm_batch = batch;
     c->warm_calls = 0;
+    c->warm_prev[0] = c->warm_prev[1] = 0;
   }
   ws->W = (float*)c->wW.p;
   ws->key = (unsigned*)c->wkey.p;
   ws->act = (unsigned long long*)c->wact.p;
-  ws->hit_call = (int*)((char*)c->wkey.p + B * 16);
+  ws->hit_call = (unsigned*)((char*)c->wkey.p + B * 16);
+  ws->stats = ws->hit_call + 1;  // [1] traffic calls, [2] hits (cumulative since the layout)
   ws->call = ++c->warm_calls;
+  c->warm_stream = s;
   return F110QP_OK;
 }
 
@@ -313,14 +331,16 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   lw->seg32 = c->lane_seg32;
   *backend = resolve_backend(c, batch, grouped) == F110QP_BACKEND_LANE ? f110qp::BACKEND_LANE
                                                                       : f110qp::BACKEND_WAVE;
-  (void)s;
   hipError_t e;
   if (c->cfg.gap_mode == F110QP_GAP_ACTIVE) {
     // counts and lists of the screen's GI list and of the fp64 re-check
     if ((e = c->hand.ensure(f110qp::kHandInts(batch) * sizeof(int))) != hipSuccess)
       return hip_fail(e, "hipMalloc gap-row lists");
     lw->hand = (int*)c->hand.p;
-    lw->screen = gap_screen(c, batch, grouped);
+    lw->recheck_all = c->recheck_all;
+    lw->screen = gap_screen(c, batch, grouped) && !c->recheck_all;
+    c->last_gap_stream = s;
+    c->last_gap_batch = batch;
     if (!lw->screen) return F110QP_OK;
   } else if (*backend == f110qp::BACKEND_WAVE) {
     return F110QP_OK;
@@ -331,6 +351,43 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   if (e != hipSuccess) return hip_fail(e, "hipMalloc lane workspace");
   lw->scratch = (double*)c->lscr.p;
   return F110QP_OK;
+}
+
+int f110qp_last_recheck_count(f110qp_ctx* c, int* count) {
+  if (!c || !count) return fail(F110QP_ERR_INVALID, "ctx / count is NULL");
+  *count = 0;
+  if (c->cfg.gap_mode != F110QP_GAP_ACTIVE || c->last_gap_batch == 0 || !c->hand.p) return F110QP_OK;
+  hipError_t e = hipStreamSynchronize(c->last_gap_stream);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  const f110qp::HandLayout H((int*)c->hand.p, c->last_gap_batch);
+  if ((e = hipMemcpy(count, H.c_rc, sizeof(int), hipMemcpyDeviceToHost)) != hipSuccess)
+    return hip_fail(e, "hipMemcpy re-check count");
+  return F110QP_OK;
+}
+
+int f110qp_warm_hits(f110qp_ctx* c, int* traffic, int* hits) {
+  if (!c || !traffic || !hits) return fail(F110QP_ERR_INVALID, "ctx / traffic / hits is NULL");
+  *traffic = 0;
+  *hits = 0;
+  if (!c->cfg.warm_start || c->warm_batch == 0 || !c->wkey.p) return F110QP_OK;
+  hipError_t e = hipStreamSynchronize(c->warm_stream);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  unsigned st[3];
+  if ((e = hipMemcpy(st, (char*)c->wkey.p + (size_t)c->warm_batch * 16, sizeof(st), hipMemcpyDeviceToHost)))
+    return hip_fail(e, "hipMemcpy warm-start counters");
+  *traffic = (int)(st[1] - c->warm_prev[0]);
+  *hits = (int)(st[2] - c->warm_prev[1]);
+  c->warm_prev[0] = st[1];
+  c->warm_prev[1] = st[2];
+  return F110QP_OK;
+}
+
+int f110qp_test_build(void) {
+#ifdef F110QP_TEST_HOOKS
+  return 1;
+#else
+  return 0;
+#endif
 }
 
 int f110qp_warm_reset(f110qp_ctx* c) {

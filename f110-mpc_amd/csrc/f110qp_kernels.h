@@ -47,8 +47,11 @@ struct WarmState {
   int ngroups = 0;
   // lane back ends: the context's call counter (from 1) and a device int holding the last call in
   // which a wave saw a key hit (see warm_traffic)
-  int* hit_call = nullptr;
-  int call = 0;
+  unsigned* hit_call = nullptr;
+  unsigned call = 0;  // wraps after 2^32 calls: compared by unsigned difference only
+  // lane back ends: cumulative counters (f110qp_warm_hits) [0] calls that moved warm traffic,
+  // [1] QPs whose key hit; one atomic per wave, and only in a call that moves the traffic
+  unsigned* stats = nullptr;
 };
 
 // Whether a lane-back-end wave moves warm-start traffic in this call (loads its QPs' keys and masks,
@@ -59,13 +62,13 @@ struct WarmState {
 // so a stream whose linearisation points repeat turns it back on within kWarmProbe calls. Without
 // hit_call (grouped / wave paths): always.
 constexpr int kWarmRecent = 2, kWarmProbe = 32;
-__device__ __forceinline__ int warm_last_hit(const WarmState& ws) {  // load early, test late
-  return ws.hit_call ? __builtin_nontemporal_load(ws.hit_call) : 0;
+__device__ __forceinline__ unsigned warm_last_hit(const WarmState& ws) {  // load early, test late
+  return ws.hit_call ? __builtin_nontemporal_load(ws.hit_call) : 0u;
 }
-__device__ __forceinline__ bool warm_traffic(const WarmState& ws, int last) {
+__device__ __forceinline__ bool warm_traffic(const WarmState& ws, unsigned last) {
   if (!ws.act || !ws.key) return false;
   if (!ws.hit_call) return true;
-  return ws.call - last <= kWarmRecent || ws.call % kWarmProbe <= 1;
+  return ws.call - last <= (unsigned)kWarmRecent || ws.call % (unsigned)kWarmProbe <= 1u;
 }
 
 // LaneWork::hand for a call of B gap-row QPs: kHandInts(B) = 3 B + 4 ints, the two counts first
@@ -95,6 +98,7 @@ struct LaneWork {
   int* hand = nullptr;  // gap rows: counts + per-QP lists (HandLayout, kHandInts(B) ints)
   int screen = 0;       // gap rows: box solve on the lane kernel first, GI only for the QPs whose
                         // box optimum violates a gap row (f110qp_kernels.hip)
+  int recheck_all = 0;  // gap rows, test build only: every QP through the fp64 re-check alone
 };
 
 // Optional per-QP objective outputs (fp64, computed in the kernels' output sweeps from the fp64

@@ -121,6 +121,14 @@ __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int*
   }
 }
 
+// The re-check list holding every QP of the call in order (the test build's F110QP_RECHECK_ALL route)
+__global__ __launch_bounds__(256) void list_all_kernel(const int B, int* __restrict__ count,
+                                                       int* __restrict__ list) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b < B) list[b] = b;
+  if (b == 0) *count = B;
+}
+
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
                         const float* xr, const float* hs, float* uo, float* xo, int* st,
                         int* its, const WarmState& ws, int backend, const LaneWork& lw,
@@ -135,6 +143,11 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
     // does not certify (SOLVED) to the re-check list, and the fp64 GI re-checks them.
     const HandLayout H(lw.hand, B);
     hipError_t e = hipSuccess;
+    if (lw.recheck_all) {  // test build: the re-check's own answer for every QP (no screen, no fp32 GI)
+      hipLaunchKernelGGL(list_all_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, H.c_rc, H.rc);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, H.rc, H.c_rc, oo, s);
+    }
     ObjOut go = oo;
     go.rc_count = H.c_rc;
     go.rc_list = H.rc;
@@ -194,7 +207,7 @@ hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const 
                                 int* its, const WarmState& gws, int* leader, int backend,
                                 const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  if (backend == BACKEND_LANE || (hs && lw.screen))  // per-QP Riccati: nothing to share
+  if (backend == BACKEND_LANE || (hs && (lw.screen || lw.recheck_all)))  // per-QP Riccati: nothing to share
     return launch_solve(P, B, x0, ul, xr, hs, uo, xo, st, its, WarmState(), backend, lw, oo, s);
   hipError_t e = hipMemsetAsync(leader, 0x7f, (size_t)gws.ngroups * sizeof(int), s);
   if (e != hipSuccess) return e;

@@ -25,10 +25,13 @@ F110QP_GI64_INSTANTIATE(F110QP_GI64_NUM)
 
 #if defined(F110QP_GI64_LAUNCH) || defined(F110QP_GI64_ALL)
 // Grid of the re-check: a grid-stride loop over the device-side count processes every listed QP,
-// whatever the grid. A call whose list is empty (the usual case) costs the launch of workgroups
-// that read a zero count and exit: 4.7 us at 256 workgroups on C3 (rocprof, round 5).
+// whatever the grid. One workgroup per CU (256 on the MI355X; the N = 48 instantiation's 154 KiB of
+// LDS fits one per CU anyway), so a long list (stiff batches list a few percent of their QPs at
+// ~170 us per heavy QP) spreads over the whole chip instead of 1/8 of it. A call whose list is
+// empty (the usual case) costs the launch of workgroups that read a zero count and exit: 4.7 us at
+// 256 workgroups against 4.45 at 32 on C3 (rocprof, round 5).
 #ifndef F110QP_RECHECK_GRID
-#define F110QP_RECHECK_GRID 32
+#define F110QP_RECHECK_GRID 256
 #endif
 constexpr int kRecheckGrid = F110QP_RECHECK_GRID;
 

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
   const int N = P.N;
   const int n3 = 3 * N;
   const int R = (2 * N + 63) / 64;  // register-row count of the wave kernel's act layout
-  const int wlast = warm_last_hit(ws);  // the warm-start traffic switch (warm_traffic)
+  const unsigned wlast = warm_last_hit(ws);  // the warm-start traffic switch (warm_traffic)
 
   // ---- stage the wave's reference paths (nq rows of 3S floats, the first 3N of each used) ---
   // Linear, coalesced sweep over the rows' first 3N entries (element e = q 3N + c -> stg[c L + q],
@@ -276,6 +276,11 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
     // kernel to reuse).
     const bool hit = wkey.w != 0u && wkey.x == kth && wkey.y == kv && wkey.z == kd;
     if (ws.hit_call && __ballot(hit) != 0ull && lane == 0) *ws.hit_call = ws.call;
+    if (ws.stats && wt) {  // f110qp_warm_hits: traffic calls (wave 0), hits (owner lanes)
+      const unsigned nh = (unsigned)__popcll(__ballot(hit && owner));
+      if (lane == 0 && nh) atomicAdd(ws.stats + 1, nh);
+      if (lane == 0 && blockIdx.x == 0) atomicAdd(ws.stats, 1u);
+    }
     const unsigned long long lo0 = hit ? wact[0] : 0ull, hi0 = hit ? wact[1] : 0ull;
     const unsigned long long lo1 = hit ? wact[2] : 0ull, hi1 = hit ? wact[3] : 0ull;
     // (a cold start from the free set beats seeding the inputs whose u_des sits on a bound:

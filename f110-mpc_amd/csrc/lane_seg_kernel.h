@@ -135,7 +135,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   // per-QP inputs and the warm-start traffic switch (warm_traffic), issued before the staging loads
   const float fX0 = x0g[3 * b + 0], fY0 = x0g[3 * b + 1], fTH0 = x0g[3 * b + 2];
   const float fv = ulg[2 * b + 0], fd = ulg[2 * b + 1];
-  const int wlast = warm_last_hit(ws);
+  const unsigned wlast = warm_last_hit(ws);
   // ---- stage the wave's reference paths (float, [3N][L]) into the scratch region ----
   // Element e = q 3N + c of the wave's nq rows (row stride 3 xr_stride in HBM) goes to
   // stg[c L + q]. (q, c) advance by 64 elements per step without a division, every load reads a
@@ -250,6 +250,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     const bool hit = wt && key3 != 0u && key0 == kth && key1 == kv && key2 == kd;
 #endif
     if (ws.hit_call && __ballot(hit) != 0ull && lane == 0) *ws.hit_call = ws.call;
+    if (ws.stats && wt) {  // f110qp_warm_hits: traffic calls (wave 0), hits (one lane per QP)
+      const unsigned nh = (unsigned)__popcll(__ballot(hit && qowner));
+      if (lane == 0 && nh) atomicAdd(ws.stats + 1, nh);
+      if (lane == 0 && blockIdx.x == 0) atomicAdd(ws.stats, 1u);
+    }
     if (hit) {
       lo0 = ws.act[2 * R * b];
       hi0 = ws.act[2 * R * b + 1];

@@ -324,6 +324,44 @@ __device__ __forceinline__ void grad_f64(const Lin& M, const KParams& P, int lan
   }
 }
 
+// H y in fp64 (H = R + Gamma'Q Gamma, the condensed Hessian): the linear rollout of y and the
+// costate of its Q-weighted states (grad_f64 with no reference, no affine term and no u_des).
+template <int R>
+__device__ __forceinline__ void hv_f64(const Lin& M, const KParams& P, int lane, int N,
+                                       const double (&y)[R], double (&hy)[R]) {
+  Lin ML = M;
+  ML.th0 = 0.0; ML.c0 = 0.0; ML.c1 = 0.0; ML.c2 = 0.0;
+  double px[R], py[R], th[R];
+  rollout_f64<R>(ML, lane, y, px, py, th);
+  const int a = lane & 1;
+  double ex[R], ey[R], et[R], lx[R], ly[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int k = 32 * r + (lane >> 1);
+    const bool contrib = (a == 1) && (k < N);
+    const double i = (double)(k + 1);
+    ex[r] = contrib ? P.q[0] * px[r] : 0.0;
+    ey[r] = contrib ? P.q[1] * py[r] : 0.0;
+    et[r] = contrib ? P.q[2] * th[r] : 0.0;
+    lx[r] = i * ex[r];
+    ly[r] = i * ey[r];
+  }
+  scan_suffix_incl_R<R>(ex);
+  scan_suffix_incl_R<R>(lx);
+  scan_suffix_incl_R<R>(ey);
+  scan_suffix_incl_R<R>(ly);
+  scan_suffix_incl_R<R>(et);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int k = 32 * r + (lane >> 1);
+    const double i = (double)(k + 1);
+    const double lth = et[r] + ML.a02 * (lx[r] - i * ex[r]) + ML.a12 * (ly[r] - i * ey[r]);
+    const double hv = a ? (P.r[1] * y[r] + ML.b21 * lth)
+                        : (P.r[0] * y[r] + ML.b00 * ex[r] + ML.b10 * ey[r] + ML.b20 * lth);
+    hy[r] = (k < N) ? hv : 0.0;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // shared memory of one wave / one QP
 // ------------------------------------------------------------------------------------------
@@ -736,16 +774,17 @@ __device__ __forceinline__ void matvec_T(Smem<NUM, GAP>& sm, const float (&h)[R]
 // dt = 0.01, so up to four, stopping once the fp32 correction is at its noise level.
 constexpr int kRefineSteps = 4;
 constexpr float kRefineTol = 2e-6f;
-// GI's final point (gap rows): refined until its fp64 KKT residual certifies it (at most
-// kRefineMax residual evaluations), then certified by strong convexity. For a point u that
-// satisfies every row (fp64, 1e-9 relative) and holds its active rows at equality, with
-// rho = H u + g - N_A mu+ (multipliers clamped at 0) and the optimum u*, e = u - u* has
-// e'He <= rho'e <= |rho|_W |e|_H (W = H^-1), so |e|_2 <= |e|_H / sqrt(lambda) <= |rho|_W / sqrt(lambda)
-// with lambda = min(r) <= lambda_min(H) (H = R + Gamma'Q Gamma). SOLVED when
-// rho'W rho <= lambda (kCertTauW max(1, |u|_inf))^2; the W-norm keeps the bound at sqrt(kappa(H))
-// times the rounding of an exact point, where |rho|_2 / lambda would be kappa times (stiff QPs,
-// kappa ~ 4e5 at N = 48, dt = 0.05). Anything else is SOLVED_INACCURATE and goes to the fp64
-// re-check (gi64_kernel.h).
+// GI's final point (gap rows): refined until its fp64 KKT residual is small (at most kRefineMax
+// residual evaluations), then certified by duality. For a point u that satisfies every row to
+// 1e-9 relative (fp64), with the multipliers mu+ = max(mu, 0) of its active rows, rho = H u + g -
+// N_A mu+ and the active rows' slacks s_j+ = max(n_j'u - b_j, 0), the duality gap of the QP whose
+// rows are relaxed by u's own violations gives |u - u*'|_H^2 <= rho'W rho + 2 sum_A mu+_j s_j+
+// (W = H^-1, u*' that QP's optimum), and |e|_2 <= |e|_H / sqrt(lambda) with lambda = min(r) <=
+// lambda_min(H) (H = R + Gamma'Q Gamma). SOLVED when that bound is <= lambda (kCertTauW max(1,
+// |u|_inf))^2, with rho'W rho bounded from above in fp64 (an fp64 Hessian product corrects the
+// fp32 W's product, hv_f64). The W-norm keeps the bound at sqrt(kappa(H)) times the rounding of
+// an exact point, where |rho|_2 / lambda would be kappa times (stiff QPs, kappa ~ 4e5 at N = 48,
+// dt = 0.05). Anything else is SOLVED_INACCURATE and goes to the fp64 re-check (gi64_kernel.h).
 constexpr int kRefineMax = 8;
 constexpr double kCertTauW = 1e-6;
 // box path's fp64 PDAS (step 4a'): passes, HIK passes before the least-index rule, flips pivoted
@@ -1646,7 +1685,6 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           wave_argmin(r2n, dummy);
           return -r2n;
         };
-        bool gi_ref_ok = false;
         float prev = 3.0e38f;
         for (int rs = 0; rs < kRefineMax; rs++) {
           wsync();
@@ -1668,7 +1706,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           rsq = wave_sum(rsq);
           float r2[R];
           const float r2n = act_res(r2);
-          if (rsq <= 0.25 * thr2 && r2n <= 1e-9f) { gi_ref_ok = true; break; }
+          if (rsq <= 0.25 * thr2 && r2n <= 1e-9f) break;  // small enough: the certificate decides below
           if (rs + 1 == kRefineMax) break;
           // v1_j = n_j' w1 (= V_j' r1 with the gap rows' stored V_j = W n_j: r1 is still in sm.vec
           // from the W product, so no rollout of w1 and no barrier)
@@ -1770,16 +1808,24 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
         wave_argmin(best64, bid64);
         STAMP_ACC(acc_refine, t_ref0);
         if (bid64 == 0x7fffffff || reentries >= 4) {
-          // certificate: refined to the residual bound, every row holds; a negative multiplier
-          // enters clamped at 0 (its row's pull stays in the residual, in primal units / lambda)
-          bool cert = gi_ref_ok && bid64 == 0x7fffffff;
+          // certificate: every row holds (fp64, the test above), evaluated at the final u64 with
+          // the multipliers clamped at 0 whatever the refinement did (a negative multiplier's pull
+          // stays in the residual, in primal units / lambda)
+          bool cert = false;
           bool neg = false;
 #pragma unroll
           for (int r = 0; r < R; r++) neg = neg || (64 * r + lane < q && sm.cmult[slot_id[r]] < 0.0);
-          // The residual bound itself, at the final u64 with the multipliers clamped at 0, when the
-          // refinement stopped short of its own test (stalled or at kRefineMax: the bound does not
-          // care how the point was reached) or a multiplier is negative
-          if (bid64 == 0x7fffffff && (!gi_ref_ok || __ballot(neg) != 0ull)) {
+          if (bid64 == 0x7fffffff) {
+            // With mu+ = max(mu, 0) on the active rows and rho = H u + g - N_A mu+, the duality gap
+            // of the QP whose rows are relaxed by u's own violation of them (at most the 1e-9
+            // relative of the feasibility test) bounds the distance to that QP's optimum u*':
+            //   |u - u*'|_H^2 <= rho'W rho + 2 sum_A mu+_j s_j+,  s_j+ = max(n_j'u - b_j, 0),
+            // and |e|_2^2 <= |e|_H^2 / lambda (lambda = min r <= lambda_min(H)). rho'W rho is bounded
+            // from above in fp64 whatever the accuracy of the fp32 W (kappa ~ 4e5 on the stiff
+            // corners): with y = W rho (the fp32 product) and r = rho - H y (fp64 Hessian product),
+            //   rho'H^-1 rho = y'(2 rho - H y) + r'H^-1 r <= y'(2 rho - H y) + |r|_2^2 / lambda,
+            // with one correction y += W r when that bound is loose (round-5 ADVICE: the fp32
+            // estimate rho'W rho and the dropped active-row term are no longer trusted).
             double r1c[R];
             wsync();
             kkt_res(true, r1c);
@@ -1793,11 +1839,41 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
             float wc[R], r2c[R];
             matvec_W<NUM, GAP, R>(sm, lane, wc);
             const float r2nc = act_res(r2c);
-            double rsq = 0.0;
+            double actg = 0.0;  // sum_A mu+_j s_j+
 #pragma unroll
-            for (int r = 0; r < R; r++) rsq += valid[r] ? r1c[r] * (double)wc[r] : 0.0;
-            rsq = wave_sum(rsq);
-            cert = rsq <= thr2 && r2nc <= 1e-9f;
+            for (int r = 0; r < R; r++)
+              if (64 * r + lane < q) actg += fmax(sm.cmult[slot_id[r]], 0.0) * fmax((double)r2c[r], 0.0);
+            actg = wave_sum(actg);
+            const double lam = fmin(P.r[0], P.r[1]);
+            double ycr[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) ycr[r] = valid[r] ? (double)wc[r] : 0.0;
+            double bound = 0.0;
+            for (int pass = 0; pass < 2; pass++) {
+              double hy[R], rr[R];
+              hv_f64<R>(M, P, lane, N, ycr, hy);
+              double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+              for (int r = 0; r < R; r++) {
+                rr[r] = valid[r] ? r1c[r] - hy[r] : 0.0;
+                t1 += valid[r] ? ycr[r] * (2.0 * r1c[r] - hy[r]) : 0.0;
+                t2 += rr[r] * rr[r];
+              }
+              t1 = wave_sum(t1);
+              t2 = wave_sum(t2);
+              bound = t1 + t2 / lam;
+              // decided: certified, or even a perfect y (bound -> t1) could not certify
+              if (pass == 1 || bound + 2.0 * actg <= thr2 || t1 + 2.0 * actg > thr2) break;
+              wsync();
+#pragma unroll
+              for (int r = 0; r < R; r++) sm.vec[vv[r]] = (float)rr[r];
+              wsync();
+              float dy[R];
+              matvec_W<NUM, GAP, R>(sm, lane, dy);
+#pragma unroll
+              for (int r = 0; r < R; r++) ycr[r] += valid[r] ? (double)dy[r] : 0.0;
+            }
+            cert = bound >= 0.0 && bound + 2.0 * actg <= thr2 && r2nc <= 1e-9f;
           }
           if constexpr (GAP) {
             // Negative-multiplier re-entry: the refined set holds a row with a negative multiplier

@@ -12,8 +12,12 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# F110QP_LIB selects a diagnostic build (e.g. lib_stamps/); default is the in-tree library
+# F110QP_LIB selects a diagnostic build (e.g. lib_stamps/); default is the in-tree product library
 LIB_PATH = os.environ.get("F110QP_LIB", os.path.join(PKG_ROOT, "lib", "libf110qp.so"))
+# the test / measurement build (same kernels; f110qp_create also reads the F110QP_* knobs that force
+# kernel variants). Solvers use it while USE_TEST_BUILD is true (the tests' `knob` fixture sets it).
+TEST_LIB_PATH = os.environ.get("F110QP_TEST_LIB", os.path.join(PKG_ROOT, "lib_test", "libf110qp.so"))
+USE_TEST_BUILD = False
 
 OK = 0
 ERR_INVALID = -1
@@ -85,6 +89,9 @@ EXPORTED = (
     "f110qp_backend_info",
     "f110qp_lane_segments",
     "f110qp_gap_screen",
+    "f110qp_last_recheck_count",
+    "f110qp_warm_hits",
+    "f110qp_test_build",
 )
 SCRATCH_NAMES = {0: "none (wave back end)", 1: "LDS fp64", 2: "LDS fp32", 3: "HBM fp64", 4: "HBM fp32"}
 
@@ -125,17 +132,18 @@ class F110QPError(RuntimeError):
     pass
 
 
-_lib = None
+_libs = {}
 
 
-def load():
-    """Load libf110qp.so (raises if it is missing: there is no fallback path)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise F110QPError(f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` (hipcc, gfx950)")
-    L = C.CDLL(LIB_PATH)
+def load(test: bool = False):
+    """Load libf110qp.so (raises if it is missing: there is no fallback path). test=True: the
+    test / measurement build lib_test/libf110qp.so."""
+    path = TEST_LIB_PATH if test else LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise F110QPError(f"{path} not built: run `make -C {PKG_ROOT}` (hipcc, gfx950)")
+    L = C.CDLL(path)
     fp = C.c_void_p
     L.f110qp_version.restype = C.c_int
     L.f110qp_last_error.restype = C.c_char_p
@@ -155,6 +163,9 @@ def load():
     L.f110qp_backend_info.argtypes = [C.c_void_p, C.c_int, C.c_int] + [C.POINTER(C.c_int)] * 3
     L.f110qp_lane_segments.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.f110qp_gap_screen.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    L.f110qp_last_recheck_count.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    L.f110qp_warm_hits.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.f110qp_test_build.restype = C.c_int
     L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
     L.f110qp_warm_reset.argtypes = [C.c_void_p]
     L.f110qp_qp_dims.argtypes = [C.c_int] + [C.POINTER(C.c_int)] * 4
@@ -169,17 +180,17 @@ def load():
     L.f110qp_parse_waypoints.argtypes = [C.c_char_p, fp, C.c_int, C.POINTER(C.c_int)]
     L.f110qp_plan_batch_dev.argtypes = [C.POINTER(PlanConfig), C.c_int, fp, fp, C.c_int, C.c_float, C.c_float,
                                         C.c_float, fp, fp, C.c_int, fp, fp, fp, fp, fp, fp, fp, fp]
-    _lib = L
+    _libs[path] = L
     return L
 
 
-def last_error() -> str:
-    return load().f110qp_last_error().decode()
+def last_error(lib=None) -> str:
+    return (lib or load()).f110qp_last_error().decode()
 
 
-def _check(rc: int, what: str):
+def _check(rc: int, what: str, lib=None):
     if rc != OK:
-        raise F110QPError(f"{what} failed ({rc}): {last_error()}")
+        raise F110QPError(f"{what} failed ({rc}): {last_error(lib)}")
 
 
 def default_config(horizon: int, **over) -> Config:
@@ -247,11 +258,12 @@ class Solver:
     """One f110qp context (device workspace). Mirrors the reference's OsqpEigen::Solver
     member of MPC (include/f110-mpc/mpc.h:63) for B instances at once."""
 
-    def __init__(self, config: Config):
-        self.lib = load()
+    def __init__(self, config: Config, test_build: bool | None = None):
+        self.lib = load(USE_TEST_BUILD if test_build is None else test_build)
         self.config = config
         h = C.c_void_p()
-        _check(self.lib.f110qp_create(C.byref(h), C.byref(config)), "f110qp_create")
+        self._chk = lambda rc, what: _check(rc, what, self.lib)
+        self._chk(self.lib.f110qp_create(C.byref(h), C.byref(config)), "f110qp_create")
         self._h = h
 
     @property
@@ -272,7 +284,7 @@ class Solver:
     def backend_info(self, batch: int, grouped: bool = False):
         """(backend, qps_per_wave, scratch) of a solve call of `batch` QPs (f110qp_backend_info)."""
         v = [C.c_int() for _ in range(3)]
-        _check(self.lib.f110qp_backend_info(self._h, int(batch), int(grouped), *[C.byref(x) for x in v]),
+        self._chk(self.lib.f110qp_backend_info(self._h, int(batch), int(grouped), *[C.byref(x) for x in v]),
                "f110qp_backend_info")
         return tuple(x.value for x in v)
 
@@ -280,14 +292,31 @@ class Solver:
         """Horizon segments per QP of a solve call of `batch` QPs (f110qp_lane_segments): 1, or
         2 / 4 / 8 when the lane back end runs the partitioned Riccati (lane_seg_kernel.h)."""
         v = C.c_int()
-        _check(self.lib.f110qp_lane_segments(self._h, int(batch), C.byref(v)), "f110qp_lane_segments")
+        self._chk(self.lib.f110qp_lane_segments(self._h, int(batch), C.byref(v)), "f110qp_lane_segments")
         return v.value
+
+    def last_recheck_count(self) -> int:
+        """QPs the last gap-row call sent to the fp64 re-check (f110qp_last_recheck_count;
+        synchronises with that call)."""
+        v = C.c_int()
+        self._chk(self.lib.f110qp_last_recheck_count(self._h, C.byref(v)), "f110qp_last_recheck_count")
+        return v.value
+
+    def warm_hits(self):
+        """(traffic_calls, hits) since the previous warm_hits (f110qp_warm_hits)."""
+        t, h = C.c_int(), C.c_int()
+        self._chk(self.lib.f110qp_warm_hits(self._h, C.byref(t), C.byref(h)), "f110qp_warm_hits")
+        return t.value, h.value
+
+    @property
+    def test_build(self) -> bool:
+        return bool(self.lib.f110qp_test_build())
 
     def gap_screen(self, batch: int) -> bool:
         """Does a gap-row solve call of `batch` QPs take the box screen on the lane back end before
         the wave kernel's GI (f110qp_gap_screen)?"""
         v = C.c_int()
-        _check(self.lib.f110qp_gap_screen(self._h, int(batch), C.byref(v)), "f110qp_gap_screen")
+        self._chk(self.lib.f110qp_gap_screen(self._h, int(batch), C.byref(v)), "f110qp_gap_screen")
         return bool(v.value)
 
     def solve(self, x0, u_lin, x_ref, halfspace=None, objective=False):
@@ -308,10 +337,10 @@ class Solver:
         if objective:
             ob = np.empty(B, np.float64)
             co = np.empty(B, np.float64)
-            _check(self.lib.f110qp_solve_batch_ex(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(u), _p(x),
+            self._chk(self.lib.f110qp_solve_batch_ex(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(u), _p(x),
                                                   _p(st), _p(it), _p(ob), _p(co)), "f110qp_solve_batch_ex")
             return u, x, st, it, ob, co
-        _check(self.lib.f110qp_solve_batch(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(u), _p(x),
+        self._chk(self.lib.f110qp_solve_batch(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(u), _p(x),
                                            _p(st), _p(it)), "f110qp_solve_batch")
         return u, x, st, it
 
@@ -342,12 +371,12 @@ class Solver:
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
         if obj is not None or cost is not None:
-            _check(self.lib.f110qp_solve_batch_ex_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
+            self._chk(self.lib.f110qp_solve_batch_ex_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
                                                       _tp(u_out), _tp(x_out), _tp(status), _tp(iters), _tp(obj),
                                                       _tp(cost), C.c_void_p(stream.cuda_stream)),
                    "f110qp_solve_batch_ex_dev")
             return
-        _check(self.lib.f110qp_solve_batch_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
+        self._chk(self.lib.f110qp_solve_batch_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
                                                _tp(u_out), _tp(x_out), _tp(status), _tp(iters),
                                                C.c_void_p(stream.cuda_stream)), "f110qp_solve_batch_dev")
 
@@ -369,7 +398,7 @@ class Solver:
         def launch():
             rc = fn(*args)
             if rc != OK:
-                _check(rc, "f110qp_solve_batch_dev")
+                _check(rc, "f110qp_solve_batch_dev", self.lib)
         return launch
 
     def prepare_grouped_dev(self, x0, u_lin, x_ref, halfspace, group, num_groups, u_out, x_out, status,
@@ -387,7 +416,7 @@ class Solver:
         def launch():
             rc = fn(*args)
             if rc != OK:
-                _check(rc, "f110qp_solve_grouped_dev")
+                _check(rc, "f110qp_solve_grouped_dev", self.lib)
         return launch
 
     def assemble_debug(self, x0, u_lin, x_ref, halfspace=None):
@@ -412,7 +441,7 @@ class Solver:
                "u": torch.empty(m, dtype=torch.float64, device=dev)}
         stream = torch.cuda.current_stream(dev)
         o = out
-        _check(self.lib.f110qp_assemble_debug_dev(self._h, _tp(x0d), _tp(uld), _tp(xrd), _tp(hsd), _tp(o["P_colptr"]),
+        self._chk(self.lib.f110qp_assemble_debug_dev(self._h, _tp(x0d), _tp(uld), _tp(xrd), _tp(hsd), _tp(o["P_colptr"]),
                                                   _tp(o["P_rowind"]), _tp(o["P_val"]), _tp(o["q"]), _tp(o["A_colptr"]),
                                                   _tp(o["A_rowind"]), _tp(o["A_val"]), _tp(o["l"]), _tp(o["u"]),
                                                   C.c_void_p(stream.cuda_stream)), "f110qp_assemble_debug_dev")
@@ -438,10 +467,10 @@ class Solver:
         if objective:
             ob = np.empty(B, np.float64)
             co = np.empty(B, np.float64)
-            _check(self.lib.f110qp_solve_grouped_ex(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(g), G, _p(u),
+            self._chk(self.lib.f110qp_solve_grouped_ex(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(g), G, _p(u),
                                                     _p(x), _p(st), _p(it), _p(ob), _p(co)), "f110qp_solve_grouped_ex")
             return u, x, st, it, ob, co
-        _check(self.lib.f110qp_solve_grouped(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(g), G, _p(u), _p(x),
+        self._chk(self.lib.f110qp_solve_grouped(self._h, B, _p(x0), _p(ul), _p(xr), _p(hs), _p(g), G, _p(u), _p(x),
                                              _p(st), _p(it)), "f110qp_solve_grouped")
         return u, x, st, it
 
@@ -455,18 +484,18 @@ class Solver:
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
         if obj is not None or cost is not None:
-            _check(self.lib.f110qp_solve_grouped_ex_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
+            self._chk(self.lib.f110qp_solve_grouped_ex_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
                                                         _tp(group), int(num_groups), _tp(u_out), _tp(x_out),
                                                         _tp(status), _tp(iters), _tp(obj), _tp(cost),
                                                         C.c_void_p(stream.cuda_stream)), "f110qp_solve_grouped_ex_dev")
             return
-        _check(self.lib.f110qp_solve_grouped_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
+        self._chk(self.lib.f110qp_solve_grouped_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(halfspace),
                                                  _tp(group), int(num_groups), _tp(u_out), _tp(x_out), _tp(status),
                                                  _tp(iters), C.c_void_p(stream.cuda_stream)),
                "f110qp_solve_grouped_dev")
 
     def warm_reset(self):
-        _check(self.lib.f110qp_warm_reset(self._h), "f110qp_warm_reset")
+        self._chk(self.lib.f110qp_warm_reset(self._h), "f110qp_warm_reset")
 
     def condense_debug_dev(self, x0, u_lin, x_ref, H_out, g_out, stream=None):
         import torch
@@ -474,7 +503,7 @@ class Solver:
         B = x0.shape[0]
         if stream is None:
             stream = torch.cuda.current_stream(x0.device)
-        _check(self.lib.f110qp_condense_debug_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(H_out),
+        self._chk(self.lib.f110qp_condense_debug_dev(self._h, B, _tp(x0), _tp(u_lin), _tp(x_ref), _tp(H_out),
                                                   _tp(g_out), C.c_void_p(stream.cuda_stream)),
                "f110qp_condense_debug_dev")
 

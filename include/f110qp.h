@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define F110QP_API_VERSION 5
+#define F110QP_API_VERSION 6
 
 /* return codes */
 #define F110QP_OK 0
@@ -142,6 +142,11 @@ typedef struct {
                     /*    Slot b of call t+1 continues slot b of call t (same batch size). */
                     /*    The lane back ends move this state only while keys hit (within  */
                     /*    the last 2 calls, or on 2 probe calls in every 32).             */
+                    /*    A stream whose linearisation point changes every tick (the      */
+                    /*    closed loop of configs[4]: theta0 follows the plant) never hits: */
+                    /*    its solves are cold solves (no factor or active set is reused;  */
+                    /*    the previous tick's active set measured a worse seed than none, */
+                    /*    DESIGN.md 2b). f110qp_warm_hits reports what a call reused.      */
   int backend;      /* F110QP_BACKEND_AUTO | _WAVE | _LANE (both give the exact optimum)    */
   int x_ref_points; /* points per QP in x_ref, >= N (0 = N). MPC::Update receives the whole   */
                     /* miniPath and reads its first N states (mpc.cpp:223-228): pass the      */
@@ -254,6 +259,25 @@ int f110qp_gap_screen(f110qp_ctx* ctx, int batch, int* on);
 
 /* Forget the warm-start state of every slot (the next call solves cold). */
 int f110qp_warm_reset(f110qp_ctx* ctx);
+
+/* What the solve calls on this context did with the warm-start state (config.warm_start) since
+ * the previous f110qp_warm_hits (or since the state was laid out for the batch size): *traffic =
+ * the calls that loaded and stored the slots' keys and active sets (the lane back ends skip both
+ * while no key hits, see warm_start), *hits = the QPs whose slot key equalled their linearisation
+ * point, i.e. that started from the slot's previous active set. Counted by the lane back ends'
+ * kernels (the wave back end reports 0); synchronises with the last warm call's stream; both 0
+ * without warm_start. */
+int f110qp_warm_hits(f110qp_ctx* ctx, int* traffic, int* hits);
+
+/* Gap rows: how many QPs the last gap-row solve call on this context sent to the fp64
+ * Goldfarb-Idnani re-check (the QPs whose fp32 GI answer the fp64
+ * certificate did not accept). Synchronises with that call's stream; 0 before any gap-row call. */
+int f110qp_last_recheck_count(f110qp_ctx* ctx, int* count);
+
+/* 1 for the test / measurement build (lib_test/libf110qp.so, -DF110QP_TEST_HOOKS), whose
+ * f110qp_create also reads create-time F110QP_* knobs from the environment that force kernel
+ * variants for the tests; 0 for the product library, which reads no environment variable. */
+int f110qp_test_build(void);
 
 /* Debug/parity hook: the condensed Hessian H [B][2N][2N] and gradient g [B][2N] exactly as
  * the solve kernel builds them on the device (float64), for comparison with the CPU oracle's

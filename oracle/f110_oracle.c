@@ -75,9 +75,28 @@ void f110o_simulate_dynamics(const double s[3], const double u[2], double dt, do
 /* ------------------------------------------------------------------------------------------ */
 /* follow-the-gap half spaces (constraints.cpp:116-265), float32 members as in the class     */
 /* ------------------------------------------------------------------------------------------ */
+/* float_trig selects the overload the reference's unqualified cos(angle1) / sin(angle1) on a float
+ * angle (:182-186) resolves to: 0 = ::cos(double) (the C library function; the restatement's
+ * default), 1 = the float overload std::cos(float) (= cosf, the product ranges * cosf in float),
+ * which the libstdc++ <math.h> wrapper puts in the global namespace when some header of the ROS /
+ * Eigen include chain pulls it in. Which one the reference build gets cannot be checked here
+ * (ROS and Eigen are absent); tests/test_halfspace_overload.py measures the difference. */
+int f110o_find_half_spaces_trig(const double state[3], const float* ranges, int nr, float angle_min,
+                                float angle_inc, float angle_max, float ftg_thresh, float divider,
+                                float buffer, double l1[3], double l2[3], int* out_lo, int* out_hi,
+                                int float_trig);
+
 int f110o_find_half_spaces(const double state[3], const float* ranges, int nr, float angle_min,
                            float angle_inc, float angle_max, float ftg_thresh, float divider,
                            float buffer, double l1[3], double l2[3], int* out_lo, int* out_hi) {
+  return f110o_find_half_spaces_trig(state, ranges, nr, angle_min, angle_inc, angle_max, ftg_thresh,
+                                     divider, buffer, l1, l2, out_lo, out_hi, 0);
+}
+
+int f110o_find_half_spaces_trig(const double state[3], const float* ranges, int nr, float angle_min,
+                                float angle_inc, float angle_max, float ftg_thresh, float divider,
+                                float buffer, double l1[3], double l2[3], int* out_lo, int* out_hi,
+                                int float_trig) {
   int num_scans = (int)((angle_max - angle_min) / angle_inc + 1); /* :118 */
   if (num_scans > nr) num_scans = nr;
   int max_gap = -1, best_lo = 0, best_hi = 0, lo = -1, hi = -1; /* :119-123 */
@@ -106,10 +125,20 @@ int f110o_find_half_spaces(const double state[3], const float* ranges, int nr, f
   if (best_lo < 0 || best_hi < 0 || best_lo >= nr || best_hi >= nr) return -1; /* quirk (i) */
   float angle1 = angle_min + best_lo * angle_inc + current_angle; /* :179 */
   float angle2 = angle_min + best_hi * angle_inc + current_angle; /* :180 */
-  float p1x = (float)(ranges[best_lo] * cos((double)angle1) + poseX); /* :182 */
-  float p1y = (float)(ranges[best_lo] * sin((double)angle1) + poseY); /* :183 */
-  float p2x = (float)(ranges[best_hi] * cos((double)angle2) + poseX); /* :185 */
-  float p2y = (float)(ranges[best_hi] * sin((double)angle2) + poseY); /* :186 */
+  float p1x, p1y, p2x, p2y;
+  if (!float_trig) {
+    p1x = (float)(ranges[best_lo] * cos((double)angle1) + poseX); /* :182 */
+    p1y = (float)(ranges[best_lo] * sin((double)angle1) + poseY); /* :183 */
+    p2x = (float)(ranges[best_hi] * cos((double)angle2) + poseX); /* :185 */
+    p2y = (float)(ranges[best_hi] * sin((double)angle2) + poseY); /* :186 */
+  } else { /* float overload: float product, then + double pose */
+    const float t1x = ranges[best_lo] * cosf(angle1), t1y = ranges[best_lo] * sinf(angle1);
+    const float t2x = ranges[best_hi] * cosf(angle2), t2y = ranges[best_hi] * sinf(angle2);
+    p1x = (float)((double)t1x + poseX);
+    p1y = (float)((double)t1y + poseY);
+    p2x = (float)((double)t2x + poseX);
+    p2y = (float)((double)t2y + poseY);
+  }
   float px = (float)poseX, py = (float)poseY;                         /* :188-189 */
   float a1 = py - p1y, b1 = p1x - px, c1 = px * p1y - py * p1x;       /* :233-235 */
   if (a1 * p2x + b1 * p2y + c1 < 0) { a1 = -a1; b1 = -b1; c1 = -c1; } /* :237-242 */

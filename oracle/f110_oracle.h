@@ -57,6 +57,11 @@ int f110o_find_half_spaces(const double state[3], const float* ranges, int num_r
                            float angle_min, float angle_increment, float angle_max,
                            float ftg_thresh, float divider, float buffer, double l1[3],
                            double l2[3], int* best_lo, int* best_hi);
+/* the same with the float overload of cos / sin at :182-186 (float_trig = 1), see f110_oracle.c */
+int f110o_find_half_spaces_trig(const double state[3], const float* ranges, int num_ranges,
+                           float angle_min, float angle_increment, float angle_max,
+                           float ftg_thresh, float divider, float buffer, double l1[3],
+                           double l2[3], int* best_lo, int* best_hi, int float_trig);
 
 /* Dimensions of the reference QP (mpc.cpp:26-29). */
 int f110o_num_variables(int horizon);

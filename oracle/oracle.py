@@ -96,6 +96,8 @@ def lib():
         L.f110o_simulate_dynamics.argtypes = [dp, dp, C.c_double, dp]
         L.f110o_find_half_spaces.argtypes = [dp, fp, C.c_int, C.c_float, C.c_float, C.c_float,
                                              C.c_float, C.c_float, C.c_float, dp, dp, ip, ip]
+        L.f110o_find_half_spaces_trig.argtypes = [dp, fp, C.c_int, C.c_float, C.c_float, C.c_float,
+                                                  C.c_float, C.c_float, C.c_float, dp, dp, ip, ip, C.c_int]
         L.f110o_assemble.argtypes = [C.POINTER(Params), dp, dp, dp, dp, C.c_int, ip, ip, dp, dp,
                                      ip, ip, dp, dp, dp]
         L.f110o_condense.argtypes = [C.POINTER(Params), dp, dp, dp, dp, dp]
@@ -167,16 +169,19 @@ def simulate_dynamics(state, inp, dt):
     return out
 
 
-def find_half_spaces(state, ranges, angle_min, angle_inc, angle_max, thresh=3.0, divider=1.5, buffer=3.0):
+def find_half_spaces(state, ranges, angle_min, angle_inc, angle_max, thresh=3.0, divider=1.5, buffer=3.0,
+                     float_trig=False):
+    """float_trig: the float overload of cos / sin at constraints.cpp:182-186 (see f110_oracle.c)."""
     s = _d(state)
     r = np.ascontiguousarray(ranges, dtype=np.float32)
     l1 = np.zeros(3)
     l2 = np.zeros(3)
     lo = C.c_int()
     hi = C.c_int()
-    rc = lib().f110o_find_half_spaces(_ptr(s), _ptr(r, C.c_float), len(r), float(angle_min), float(angle_inc),
-                                      float(angle_max), float(thresh), float(divider), float(buffer),
-                                      _ptr(l1), _ptr(l2), C.byref(lo), C.byref(hi))
+    rc = lib().f110o_find_half_spaces_trig(_ptr(s), _ptr(r, C.c_float), len(r), float(angle_min),
+                                           float(angle_inc), float(angle_max), float(thresh), float(divider),
+                                           float(buffer), _ptr(l1), _ptr(l2), C.byref(lo), C.byref(hi),
+                                           int(bool(float_trig)))
     return rc, l1, l2, lo.value, hi.value
 
 

@@ -46,3 +46,17 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.fail("GPU test selected but no HIP device is visible")
     return torch.device("cuda", 0)
+
+
+@pytest.fixture
+def knob(capi, monkeypatch):
+    """Set a create-time F110QP_* test knob (F110QP_LANE_SEG=4, ...) for the rest of the test and
+    route the test's solvers to the test build (lib_test/libf110qp.so), the only library that reads
+    them: the product library reads no environment variable (f110qp_api.cpp, test_hooks)."""
+    monkeypatch.setattr(capi, "USE_TEST_BUILD", True)
+
+    def set_knob(name, value):
+        assert name.startswith("F110QP_"), name
+        monkeypatch.setenv(name, str(value))
+
+    return set_knob

@@ -23,6 +23,35 @@ def test_library_exports_every_declared_symbol(capi):
         assert hasattr(lib, s), s
 
 
+def test_product_library_reads_no_environment(capi):
+    """The product library (what bench.py times and MPC::Update links) carries no F110QP_* knob:
+    its behaviour is the config alone, as the reference's fixed OSQP settings (src/mpc.cpp:98-99).
+    The knobs live in the test build only (lib_test/libf110qp.so, -DF110QP_TEST_HOOKS)."""
+    data = open(capi.LIB_PATH, "rb").read()
+    assert b"F110QP_" not in data
+    assert b"getenv" not in data
+    assert capi.load().f110qp_test_build() == 0
+    t = capi.load(test=True)
+    assert t.f110qp_test_build() == 1
+    assert b"F110QP_RECHECK_ALL" in open(capi.TEST_LIB_PATH, "rb").read()
+    for sym in declared_symbols():
+        assert hasattr(C.CDLL(capi.TEST_LIB_PATH), sym), sym
+
+
+def test_diagnostic_queries_without_a_call(capi):
+    """f110qp_last_recheck_count and f110qp_warm_hits before any solve call: zero, no HIP call."""
+    s = capi.Solver(capi.default_config(20, gap_mode=capi.GAP_ACTIVE))
+    assert s.last_recheck_count() == 0
+    assert s.warm_hits() == (0, 0)
+    s.close()
+    w = capi.Solver(capi.default_config(20, warm_start=1))
+    assert w.warm_hits() == (0, 0) and w.last_recheck_count() == 0
+    L = capi.load()
+    assert L.f110qp_last_recheck_count(None, None) == capi.ERR_INVALID
+    assert L.f110qp_warm_hits(w._h, None, None) == capi.ERR_INVALID
+    w.close()
+
+
 def test_library_is_gfx950_code_object(capi):
     data = open(capi.LIB_PATH, "rb").read()
     assert b"gfx950" in data  # the offload bundle targets MI355X
@@ -30,7 +59,7 @@ def test_library_is_gfx950_code_object(capi):
 
 def test_version_and_defaults(capi):
     L = capi.load()
-    assert L.f110qp_version() == 5
+    assert L.f110qp_version() == 6
     c = capi.default_config(20)
     # params.yaml:1-13,42-47 and constraints.cpp:19,21
     assert c.horizon == 20 and c.dt == np.float32(0.01)
@@ -136,7 +165,7 @@ def test_product_does_not_import_the_oracle():
 def test_capi_raises_when_library_missing(monkeypatch):
     from f110qp import capi
 
-    monkeypatch.setattr(capi, "_lib", None)
+    monkeypatch.setattr(capi, "_libs", {})
     monkeypatch.setattr(capi, "LIB_PATH", "/nonexistent/libf110qp.so")
     with pytest.raises(capi.F110QPError, match="not built"):
         capi.load()

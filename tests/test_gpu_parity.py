@@ -528,15 +528,15 @@ def test_lane_backend_custom_weights_and_far_origin(oracle, capi, be):
 @pytest.mark.parametrize("dref", ["0", "1"])
 @pytest.mark.parametrize("rot", ["0", "1"])
 @pytest.mark.parametrize("N", [20, 40])
-def test_lane_backend_heading_frame(oracle, capi, monkeypatch, rot, dref, N):
+def test_lane_backend_heading_frame(oracle, capi, knob, monkeypatch, rot, dref, N):
     """q0 == q1 (the shipped params.yaml) runs the lane kernel in the frame of the heading
     theta0 (lane_kernel.h ROT: four zero model entries); F110QP_LANE_ROT=0 forces the general
     frame. The references are converted once to fp64 offsets in LDS (DREF) where the resident
     waves fit; F110QP_LANE_DREF=0 keeps the per-stage conversion of the float staging. Every
     combination gives the exact optimum, also 1 km from the origin with headings all round the
     circle."""
-    monkeypatch.setenv("F110QP_LANE_ROT", rot)
-    monkeypatch.setenv("F110QP_LANE_DREF", dref)
+    knob("F110QP_LANE_ROT", rot)
+    knob("F110QP_LANE_DREF", dref)
     w = workload.make_batch(1500, N, seed=6060 + N, heading="true", lateral=1.5, steer_range=1.0)
     w["x0"][:, 2] = np.random.default_rng(N).uniform(-np.pi, np.pi, 1500).astype(np.float32)
     w["x0"][:, :2] += np.float32(1000.0)
@@ -547,13 +547,13 @@ def test_lane_backend_heading_frame(oracle, capi, monkeypatch, rot, dref, N):
 
 @pytest.mark.parametrize("be", RICCATI)
 @pytest.mark.parametrize("kmax,N", [("0", 20), ("1", 20), ("2", 40), ("0", 40)])
-def test_lane_backend_single_flip_fallback(oracle, capi, monkeypatch, be, kmax, N):
+def test_lane_backend_single_flip_fallback(oracle, capi, knob, monkeypatch, be, kmax, N):
     """F110QP_LANE_KMAX caps the multi-flip PDAS passes of the lane kernel; past the cap a QP
     flips one complementarity violation per pass (least index, stage-major), so the QPs with
     many active bounds finish inside the same launch in more passes. kmax = 0: single flips
     from the first pass. Results stay exact, repeated calls on one context agree, and the pass
     counts exceed the PDAS ones."""
-    monkeypatch.setenv("F110QP_LANE_KMAX", kmax)
+    knob("F110QP_LANE_KMAX", kmax)
     w = workload.make_batch(3000, N, seed=991 + N, heading="true", lateral=1.5, steer_range=1.0)
     s = capi.Solver(capi.default_config(N, backend=_be(capi, be)))
     ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"], w["u_lin"], w["x_ref"])
@@ -570,10 +570,10 @@ def test_lane_backend_single_flip_fallback(oracle, capi, monkeypatch, be, kmax, 
 
 
 @pytest.mark.parametrize("qpw", ["1", "2", "8", "64"])
-def test_lane_backend_qps_per_wave(oracle, capi, monkeypatch, qpw):
+def test_lane_backend_qps_per_wave(oracle, capi, knob, monkeypatch, qpw):
     """Every QPs-per-wave layout of the lane kernel (F110QP_LANE_QPW; auto picks by batch)
     gives the same exact results; the batch is not a multiple of the wave width."""
-    monkeypatch.setenv("F110QP_LANE_QPW", qpw)
+    knob("F110QP_LANE_QPW", qpw)
     N, B = 40, 700
     w = workload.make_batch(B, N, seed=5150, heading="true", lateral=1.2, steer_range=0.8)
     u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE, tol=2e-6)
@@ -581,11 +581,11 @@ def test_lane_backend_qps_per_wave(oracle, capi, monkeypatch, qpw):
 
 
 @pytest.mark.parametrize("cap", ["0", "1", "2"])
-def test_wave_box_pdas_cap_falls_back_to_gi(oracle, capi, monkeypatch, cap):
+def test_wave_box_pdas_cap_falls_back_to_gi(oracle, capi, knob, monkeypatch, cap):
     """F110QP_PDAS_MAX caps the wave kernel's box PDAS on the swept Hessian (0: the GI loop
     solves from the unconstrained point; 1-2: PDAS stops short on the QPs with many active
     bounds and GI restarts): the results stay exact."""
-    monkeypatch.setenv("F110QP_PDAS_MAX", cap)
+    knob("F110QP_PDAS_MAX", cap)
     N = 20
     w = workload.make_batch(600, N, seed=4242, heading="true", lateral=1.5, steer_range=1.0)
     check(oracle, capi, N, w, backend=capi.BACKEND_WAVE)
@@ -638,11 +638,11 @@ def test_lane_backend_c4_shard(oracle, capi, be):
 
 
 @pytest.mark.parametrize("mode", ["1", "2", "3", "4"])
-def test_lane_backend_scratch_modes(oracle, capi, monkeypatch, mode):
+def test_lane_backend_scratch_modes(oracle, capi, knob, monkeypatch, mode):
     """Every Riccati-scratch placement of the lane back end (LDS fp64 / LDS fp32 / HBM fp64 /
     HBM fp32, F110QP_LANE_MODE) gives the exact optimum within the tolerance; N = 40 covers
     the fall-back of LDS fp64 (too big) to HBM."""
-    monkeypatch.setenv("F110QP_LANE_MODE", mode)
+    knob("F110QP_LANE_MODE", mode)
     lo, hi = np.float32([3.0, -0.43]), np.float32([4.5, 0.43])
     for N, seed in ((20, 811), (40, 812)):
         w = workload.make_batch(1500, N, seed=seed, heading="true", lateral=1.2, steer_range=0.8)
@@ -655,15 +655,15 @@ def test_lane_backend_scratch_modes(oracle, capi, monkeypatch, mode):
 
 @pytest.mark.parametrize("be,mode,kmax", [("wave", "0", "16"), ("lane", "1", "16"), ("lane", "4", "16"),
                                            ("lane", "1", "0"), ("lane", "4", "0")])
-def test_degenerate_bound_zero_multiplier(oracle, capi, monkeypatch, be, mode, kmax):
+def test_degenerate_bound_zero_multiplier(oracle, capi, knob, monkeypatch, be, mode, kmax):
     """u_des = (4.5, 0) with des_vel = umax (params.yaml:42,46): with Q = 0 the optimum is
     u = u_des at every stage, so the speed sits exactly on its upper bound with a ZERO multiplier
     (a degenerate complementarity pair), and with a tiny Q it is within rounding of that. The
     PDAS flip tests carry a tolerance, so rounding noise cannot flip such an input free -> bound
     -> free until the pass cap (MAX_ITER): every QP must come back SOLVED at the exact optimum,
     with the multi-flip passes and with single flips from the first pass, fp64 and fp32 gains."""
-    monkeypatch.setenv("F110QP_LANE_MODE", mode)
-    monkeypatch.setenv("F110QP_LANE_KMAX", kmax)
+    knob("F110QP_LANE_MODE", mode)
+    knob("F110QP_LANE_KMAX", kmax)
     N = 20
     for q in ([0.0, 0.0, 0.0], [1e-9, 1e-9, 0.0], [1e-3, 1e-3, 0.0]):
         w = workload.make_batch(700, N, seed=4500, heading="true", lateral=0.0, steer_range=0.0)
@@ -733,11 +733,11 @@ def test_closed_loop_stream_warm(oracle, capi, be):
 
 @pytest.mark.parametrize("mode", ["0", "1", "2", "4"])
 @pytest.mark.parametrize("N", [30, 32])
-def test_lane_backend_reference_horizon_scratch(oracle, capi, monkeypatch, mode, N):
+def test_lane_backend_reference_horizon_scratch(oracle, capi, knob, monkeypatch, mode, N):
     """The reference default horizon (params.yaml:12, N = 30) and N = 32 at a C5-sized batch on
     every lane scratch placement (auto, LDS fp64, LDS fp32, HBM fp32): the auto policy's LDS
     budget near its cap stays exact. Checked on a sample against the exact optimum."""
-    monkeypatch.setenv("F110QP_LANE_MODE", mode)
+    knob("F110QP_LANE_MODE", mode)
     B = 4096
     w = workload.make_batch(B, N, seed=3030 + N, heading="true", lateral=1.0, steer_range=0.6)
     s = capi.Solver(capi.default_config(N, backend=capi.BACKEND_LANE))
@@ -969,3 +969,25 @@ def test_solve_batch_dev_sync_matches_async(capi):
         s.close()
         for a, b in zip(outs[0], outs[1]):
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("seg", ["auto", "1"])
+def test_warm_hits_report_what_a_stream_reuses(capi, knob, seg):
+    """f110qp_warm_hits counts what the lane back ends' warm start actually did: a repeated
+    linearisation point hits on every QP; a stream whose theta0 moves every tick (the configs[4]
+    closed loop) never hits, and its calls move warm traffic only for two calls after the last hit
+    and on the two probe calls in every 32 (warm_traffic, f110qp_kernels.h)."""
+    if seg == "1":
+        knob("F110QP_LANE_SEG", "1")
+    N, B = 20, 4096
+    w = workload.make_batch(B, N, seed=31)
+    s = capi.Solver(capi.default_config(N, warm_start=1, backend=capi.BACKEND_LANE))
+    s.solve(w["x0"], w["u_lin"], w["x_ref"])  # call 1: keys written, none valid yet
+    s.solve(w["x0"], w["u_lin"], w["x_ref"])  # call 2: every key repeats
+    assert s.warm_hits() == (2, B)
+    for k in range(40):  # calls 3..42: theta0 moves every call
+        w["x0"][:, 2] += np.float32(1e-3)
+        u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
+        assert (st == capi.SOLVED).all()
+    assert s.warm_hits() == (4, 0)  # calls 3, 4 (within 2 of the hit) and the probes 32, 33
+    s.close()

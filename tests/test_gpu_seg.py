@@ -18,11 +18,11 @@ def _lane(capi, N, **cfg):
 
 @pytest.mark.parametrize("S,N", [(2, 2), (2, 10), (4, 20), (2, 30), (8, 40), (4, 40), (2, 40), (8, 48), (4, 4),
                                  (8, 16), (4, 30), (8, 30), (8, 20), (4, 17), (2, 25), (8, 47), (4, 9), (2, 3)])
-def test_segments_horizons(oracle, capi, monkeypatch, S, N):
+def test_segments_horizons(oracle, capi, knob, monkeypatch, S, N):
     """Every segment count on horizons it divides and on horizons it does not (segments of
     floor(N / S) or one more stage, 2 .. 24), many active bounds on both faces, batch not a
     multiple of the QPs per wave; N / S < 2 keeps the sequential kernel."""
-    monkeypatch.setenv("F110QP_LANE_SEG", str(S))
+    knob("F110QP_LANE_SEG", str(S))
     w = workload.make_batch(1000, N, seed=9100 + 10 * S + N, heading="true", lateral=1.5, steer_range=1.0)
     s = _lane(capi, N)
     assert s.lane_segments(1000) == (S if N // S >= 2 else 1)
@@ -33,11 +33,11 @@ def test_segments_horizons(oracle, capi, monkeypatch, S, N):
 
 @pytest.mark.parametrize("rot", ["0", "1"])
 @pytest.mark.parametrize("S", ["2", "4"])
-def test_segments_general_frame_far_origin(oracle, capi, monkeypatch, rot, S):
+def test_segments_general_frame_far_origin(oracle, capi, knob, monkeypatch, rot, S):
     """Heading frame (q0 == q1) and general frame (F110QP_LANE_ROT=0), headings all round the
     circle, 1 km from the origin."""
-    monkeypatch.setenv("F110QP_LANE_SEG", S)
-    monkeypatch.setenv("F110QP_LANE_ROT", rot)
+    knob("F110QP_LANE_SEG", S)
+    knob("F110QP_LANE_ROT", rot)
     N, B = 20, 1500
     w = workload.make_batch(B, N, seed=6161, heading="true", lateral=1.5, steer_range=1.0)
     w["x0"][:, 2] = np.random.default_rng(5).uniform(-np.pi, np.pi, B).astype(np.float32)
@@ -46,9 +46,9 @@ def test_segments_general_frame_far_origin(oracle, capi, monkeypatch, rot, S):
     check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
 
 
-def test_segments_custom_weights(oracle, capi, monkeypatch):
+def test_segments_custom_weights(oracle, capi, knob, monkeypatch):
     """q0 != q1 (general frame), other R, u_des inside the box, narrow bounds."""
-    monkeypatch.setenv("F110QP_LANE_SEG", "4")
+    knob("F110QP_LANE_SEG", "4")
     N = 20
     over = dict(q=[3.0, 7.0, 2.0], r=[0.5, 1.5], u_des=[3.7, 0.05], u_min=[3.5, -0.2], u_max=[4.0, 0.2])
     w = workload.make_batch(640, N, seed=882, lateral=0.7)
@@ -56,21 +56,21 @@ def test_segments_custom_weights(oracle, capi, monkeypatch):
 
 
 @pytest.mark.parametrize("kmax,S,N", [("0", "4", 20), ("1", "4", 20), ("0", "8", 40), ("2", "2", 40)])
-def test_segments_single_flip(oracle, capi, monkeypatch, kmax, S, N):
+def test_segments_single_flip(oracle, capi, knob, monkeypatch, kmax, S, N):
     """Past kmax PDAS passes a QP flips only its first violation over the WHOLE horizon (the min
     over its segment lanes; the other segments undo theirs): exact results, more passes."""
-    monkeypatch.setenv("F110QP_LANE_SEG", S)
-    monkeypatch.setenv("F110QP_LANE_KMAX", kmax)
+    knob("F110QP_LANE_SEG", S)
+    knob("F110QP_LANE_KMAX", kmax)
     w = workload.make_batch(1200, N, seed=992 + N, heading="true", lateral=1.5, steer_range=1.0)
     u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
-    monkeypatch.setenv("F110QP_LANE_SEG", "1")
+    knob("F110QP_LANE_SEG", "1")
     s = _lane(capi, N)
     _, _, _, it_seq = s.solve(w["x0"], w["u_lin"], w["x_ref"])
     s.close()
     # the same single-flip iterates as the sequential kernel (pass counts agree)
     assert np.abs(it.astype(int) - it_seq.astype(int)).max() <= 1
     monkeypatch.delenv("F110QP_LANE_KMAX")
-    monkeypatch.setenv("F110QP_LANE_SEG", S)
+    knob("F110QP_LANE_SEG", S)
     s = _lane(capi, N)
     _, _, _, it_pdas = s.solve(w["x0"], w["u_lin"], w["x_ref"])
     s.close()
@@ -78,14 +78,14 @@ def test_segments_single_flip(oracle, capi, monkeypatch, kmax, S, N):
 
 
 @pytest.mark.parametrize("S", ["2", "4", "8"])
-def test_segments_agree_with_sequential(capi, monkeypatch, S):
+def test_segments_agree_with_sequential(capi, knob, monkeypatch, S):
     """Same PDAS iterates as lane_kernel.h (pass counts equal on all but rounding ties), same
     status, solutions within 1e-7."""
     N, B = 40, 2048
     w = workload.make_batch(B, N, seed=2222, heading="true", lateral=1.2, steer_range=0.8)
     out = {}
     for seg in ("1", S):
-        monkeypatch.setenv("F110QP_LANE_SEG", seg)
+        knob("F110QP_LANE_SEG", seg)
         s = _lane(capi, N)
         out[seg] = s.solve(w["x0"], w["u_lin"], w["x_ref"], objective=True)
         s.close()
@@ -98,10 +98,10 @@ def test_segments_agree_with_sequential(capi, monkeypatch, S):
     np.testing.assert_allclose(b[5], a[5], rtol=1e-9, atol=1e-12)
 
 
-def test_segments_objective(oracle, capi, monkeypatch):
+def test_segments_objective(oracle, capi, knob, monkeypatch):
     """obj / cost outputs (the segment lanes' partial sums reduced across the QP) against the
     oracle's objective of its exact optimum."""
-    monkeypatch.setenv("F110QP_LANE_SEG", "4")
+    knob("F110QP_LANE_SEG", "4")
     N, B = 40, 500
     w = workload.make_batch(B, N, seed=1717, heading="true", lateral=1.0, steer_range=0.6)
     s = _lane(capi, N)
@@ -139,9 +139,9 @@ def test_segments_warm_closed_loop(oracle, capi, monkeypatch):
     warm.close()
 
 
-def test_segments_non_finite(oracle, capi, monkeypatch):
+def test_segments_non_finite(oracle, capi, knob, monkeypatch):
     """NaN / inf inputs: NUMERICAL and NaN outputs on every segment of those QPs only."""
-    monkeypatch.setenv("F110QP_LANE_SEG", "4")
+    knob("F110QP_LANE_SEG", "4")
     N, B = 20, 777
     w = workload.make_batch(B, N, seed=1414)
     bad = {3: ("x_ref", (3, 17, 0), np.nan), 70: ("x0", (70, 2), np.inf), 130: ("u_lin", (130, 1), np.nan),
@@ -160,10 +160,10 @@ def test_segments_non_finite(oracle, capi, monkeypatch):
     assert rel_err(u[good], ur).max() <= TOL and rel_err(x[good], xr).max() <= TOL
 
 
-def test_segments_degenerate_bound(oracle, capi, monkeypatch):
+def test_segments_degenerate_bound(oracle, capi, knob, monkeypatch):
     """u_des on the speed bound with Q = 0: zero multipliers; the flip tolerances hold on the
     segmented kernel too."""
-    monkeypatch.setenv("F110QP_LANE_SEG", "4")
+    knob("F110QP_LANE_SEG", "4")
     N = 20
     for q in ([0.0, 0.0, 0.0], [1e-9, 1e-9, 0.0]):
         w = workload.make_batch(700, N, seed=4500, heading="true", lateral=0.0, steer_range=0.0)
@@ -172,28 +172,28 @@ def test_segments_degenerate_bound(oracle, capi, monkeypatch):
 
 
 @pytest.mark.parametrize("S,N", [("4", 20), ("8", 40), ("2", 30)])
-def test_segments_refresh_and_stored_gains_agree(oracle, capi, monkeypatch, S, N):
+def test_segments_refresh_and_stored_gains_agree(oracle, capi, knob, monkeypatch, S, N):
     """The two ways the segmented kernel applies the segment-end multiplier lam_j to the
     feed-forward: the lam-gains F_i kept in the scratch (where the LDS holds 14 doubles per stage)
     and the refresh sweep (F110QP_LANE_DREF=0 forces it): same status, solutions within 1e-6, both
     at the exact optimum."""
-    monkeypatch.setenv("F110QP_LANE_SEG", S)
+    knob("F110QP_LANE_SEG", S)
     w = workload.make_batch(900, N, seed=7300 + N, heading="true", lateral=1.2, steer_range=0.8)
     out = {}
     for dref in ("1", "0"):
-        monkeypatch.setenv("F110QP_LANE_DREF", dref)
+        knob("F110QP_LANE_DREF", dref)
         out[dref] = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
     np.testing.assert_array_equal(out["0"][2], out["1"][2])
     assert rel_err(out["1"][0], out["0"][0].astype(np.float64)).max() <= 1e-6
 
 
 @pytest.mark.parametrize("S,N", [(2, 20), (4, 20), (8, 40), (4, 40), (2, 40), (4, 30)])
-def test_segments_fp32_scratch(oracle, capi, monkeypatch, S, N):
+def test_segments_fp32_scratch(oracle, capi, knob, monkeypatch, S, N):
     """Float references and Riccati scratch (F110QP_LANE_SEG_F32=1; AUTO takes them where fp64
     does not fit, e.g. 16,384 x N = 40): many active bounds on both faces, the exact optimum within
     the fp32-gain tolerance of test_lane_backend_scratch_modes."""
-    monkeypatch.setenv("F110QP_LANE_SEG", str(S))
-    monkeypatch.setenv("F110QP_LANE_SEG_F32", "1")
+    knob("F110QP_LANE_SEG", str(S))
+    knob("F110QP_LANE_SEG_F32", "1")
     w = workload.make_batch(1000, N, seed=9300 + 10 * S + N, heading="true", lateral=1.5, steer_range=1.0)
     s = _lane(capi, N)
     assert s.lane_segments(1000) == S
@@ -205,12 +205,12 @@ def test_segments_fp32_scratch(oracle, capi, monkeypatch, S, N):
 
 
 @pytest.mark.parametrize("kmax", ["16", "0"])
-def test_segments_fp32_degenerate_bound(oracle, capi, monkeypatch, kmax):
+def test_segments_fp32_degenerate_bound(oracle, capi, knob, monkeypatch, kmax):
     """des_vel = umax with Q = 0 / tiny Q (a zero-multiplier active bound) on fp32 scratch: the
     single-flip passes' fp32 tolerance settles it (lane_kernel.h's HBM-fp32 rule)."""
-    monkeypatch.setenv("F110QP_LANE_SEG", "4")
-    monkeypatch.setenv("F110QP_LANE_SEG_F32", "1")
-    monkeypatch.setenv("F110QP_LANE_KMAX", kmax)
+    knob("F110QP_LANE_SEG", "4")
+    knob("F110QP_LANE_SEG_F32", "1")
+    knob("F110QP_LANE_KMAX", kmax)
     N = 20
     for q in ([0.0, 0.0, 0.0], [1e-9, 1e-9, 0.0], [1e-3, 1e-3, 0.0]):
         w = workload.make_batch(700, N, seed=4500, heading="true", lateral=0.0, steer_range=0.0)

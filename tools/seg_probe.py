@@ -12,6 +12,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "f110-mpc_amd"))
 from f110qp import capi, workload  # noqa: E402
+capi.USE_TEST_BUILD = True  # the F110QP_* knobs below are read by the test build only
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
