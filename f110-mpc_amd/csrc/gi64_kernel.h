@@ -21,14 +21,13 @@
 //      z = W (n_p - N_A r) with N_A r by the adjoint (costate) scans, no stored W n_j;
 //   3. the final set's equality QP solved afresh from W and the factor, then the certificate of
 //      the wave kernel (solve_kernel.h kCertTauW): every row within 1e-9 (1 + |b| + |x|_inf), and
-//      with the residual rho = H u + g - N_A mu+ (mu clamped at 0) and the active rows' slacks
-//      s_j+ = max(n_j'u - b_j, 0): B = rho'W rho (bounded from above in fp64 through an fp64
-//      Hessian product) + 2 sum_A mu+_j s_j+ <= lambda (tau max(1, |u|_inf))^2, lambda = min(R)
-//      <= lambda_min(H). B bounds |u - u*'|_H^2 (the duality gap), so |u - u*'|_2 <= tau max(1,
-//      |u|_inf) for the optimum u*' of the QP whose rows are relaxed by u's own violations (<= the
-//      1e-9 tolerance), and the QP is SOLVED, else SOLVED_INACCURATE; an empty feasible set
-//      PRIMAL_INFEASIBLE, the cap MAX_ITER, non-finite data NUMERICAL. u*, x* (fp64 rollout) and
-//      obj / cost are written.
+//      with the residual rho = H u + g - N_A mu+ (mu clamped at 0), rho'W rho (bounded from above
+//      in fp64 through an fp64 Hessian product) <= lambda (tau max(1, |u|_inf))^2, lambda = min(R)
+//      <= lambda_min(H): rho'W rho bounds |u - u*'|_H^2 (the duality gap at mu+) for the optimum u*'
+//      of the QP whose row bounds are moved by u's own residuals on them (<= the 1e-9 tolerance),
+//      so |u - u*'|_2 <= tau max(1, |u|_inf) and the QP is SOLVED, else SOLVED_INACCURATE; an empty
+//      feasible set PRIMAL_INFEASIBLE, the cap MAX_ITER, non-finite data NUMERICAL. u*, x* (fp64
+//      rollout) and obj / cost are written.
 #pragma once
 #include "solve_kernel.h"
 
@@ -659,22 +658,6 @@ __device__ void gi64_qp(G64Smem<NUM>& sm, const int b, const KParams& P, const f
     wave_sync();
     matvec_W(wr);
     wave_sync();
-    // the active rows' slacks s_j+ = max(n_j'u - b_j, 0) through the per-id table: the duality gap
-    // of the QP relaxed by u's own violations (<= the feasibility tolerance above) bounds
-    // |u - u*'|_H^2 <= rho'W rho + 2 sum_A mu+_j s_j+ (solve_kernel.h, the wave kernel's certificate)
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      sm.cid[3 * vv[r]] = valid[r] ? x[r] - lb[r] : 0.0;
-      sm.cid[3 * vv[r] + 1] = valid[r] ? ub[r] - x[r] : 0.0;
-      sm.cid[3 * vv[r] + 2] = valid[r] ? gah * px[r] + gbh * py[r] - gbe : 0.0;
-    }
-    wave_sync();
-    double actg = 0.0;
-#pragma unroll
-    for (int r = 0; r < R; r++)
-      if (64 * r + lane < q) actg += mup[r] * fmax(sm.cid[slot_id[r]], 0.0);
-    actg = wave_sum(actg);
-    wave_sync();
     // rho'W rho from above in fp64: y = W rho, rho'H^-1 rho <= y'(2 rho - H y) + |rho - H y|^2 / lambda
     const double lam = fmin(P.r[0], P.r[1]);
     double hy[R];
@@ -688,7 +671,7 @@ __device__ void gi64_qp(G64Smem<NUM>& sm, const int b, const KParams& P, const f
     }
     const double rs = wave_sum(t1) + wave_sum(t2) / lam;
     const double ctol = kCertTau * fmax(1.0, umax);
-    const bool cert = !(__ballot(viol) != 0ull) && rs >= 0.0 && rs + 2.0 * actg <= lam * ctol * ctol;
+    const bool cert = !(__ballot(viol) != 0ull) && rs >= 0.0 && rs <= lam * ctol * ctol;
     if (!cert) status = F110QP_SOLVED_INACCURATE_ID;
   }
   const bool ok = (status == F110QP_SOLVED_ID) || (status == F110QP_SOLVED_INACCURATE_ID);

@@ -141,44 +141,39 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   // stg[c L + q]. (q, c) advance by 64 elements per step without a division, every load reads a
   // valid address (clamped) and every store lands (past the staged rows for e >= tot), so the
   // loop has no EXEC-masked region: ~11 instructions per element instead of ~50 (ISA).
-  {
-    float* stg = reinterpret_cast<float*>(lbase + o_sc);
-    const int n3 = 3 * N, S3 = 3 * P.xr_stride, tot = nq * n3;
-    const float* src = xrg + (size_t)b0 * S3;
-    const int dq = 64 / n3, dc = 64 - dq * n3;
-    int q = lane / n3, c = lane - (lane / n3) * n3;
-    const int junk = n3 * L + lane;                  // inside the scratch rows, never read
-    const int last_off = (nq - 1) * S3 + (n3 - 1);  // a valid element for the clamped loads
-    constexpr int kChunk = 16;  // C5 and the C4 shard stage 960 floats per wave: one round trip
-    for (int e0 = 0; e0 < tot; e0 += kChunk * 64) {
-      float vbuf[kChunk];
-      int dst[kChunk];
+  // Chunk 0's loads are issued first and the linearisation below runs while they are in flight
+  // (it needs only the per-QP scalars above); then the chunks go to LDS.
+  const int n3s = 3 * N, S3 = 3 * P.xr_stride, tots = nq * n3s;
+  const float* const srcs = xrg + (size_t)b0 * S3;
+  const int dqs = 64 / n3s, dcs = 64 - dqs * n3s;
+  int sq = lane / n3s, scol = lane - (lane / n3s) * n3s;
+  const int junk = n3s * L + lane;                  // inside the scratch rows, never read
+  const int last_off = (nq - 1) * S3 + (n3s - 1);  // a valid element for the clamped loads
+  constexpr int kChunk = 16;  // C5 and the C4 shard stage 960 floats per wave: one round trip
+  float vbuf[kChunk];
+  int dst[kChunk];
+  auto issue = [&](int e0) __attribute__((always_inline)) {
 #pragma unroll
-      for (int j = 0; j < kChunk; j++) {
-        const bool in = e0 + j * 64 + lane < tot;
-        dst[j] = in ? c * L + q : junk;
-        vbuf[j] = src[in ? q * S3 + c : last_off];
-        q += dq;
-        c += dc;
-        const bool wrap = c >= n3;
-        c -= wrap ? n3 : 0;
-        q += wrap ? 1 : 0;
-      }
-#pragma unroll
-      for (int j = 0; j < kChunk; j++) stg[dst[j]] = vbuf[j];
+    for (int j = 0; j < kChunk; j++) {
+      const bool in = e0 + j * 64 + lane < tots;
+      dst[j] = in ? scol * L + sq : junk;
+      vbuf[j] = srcs[in ? sq * S3 + scol : last_off];
+      sq += dqs;
+      scol += dcs;
+      const bool wrap = scol >= n3s;
+      scol -= wrap ? n3s : 0;
+      sq += wrap ? 1 : 0;
     }
-    __syncthreads();
-  }
-  // the warm-start key, when this call moves warm traffic (wlast arrived with the staging loads; the
-  // key's round trip overlaps the linearisation below)
+  };
+  issue(0);
+  // the warm-start key, when this call moves warm traffic (its round trip, like the staging
+  // loads', overlaps the linearisation below)
   const bool wt = warm_traffic(ws, wlast);
   unsigned key0 = 0u, key1 = 0u, key2 = 0u, key3 = 0u;
   if (wt) {
     const uint4 k4 = *reinterpret_cast<const uint4*>(ws.key + 4 * (size_t)b);
     key0 = k4.x; key1 = k4.y; key2 = k4.z; key3 = k4.w;
   }
-
-  SSTAMP(t_stg);
   // ---- per-lane QP data (Model::Linearize, model.cpp:30-59), as lane_kernel.h ----
   const double X0 = (double)fX0, Y0 = (double)fY0;
   const double th0 = (double)fTH0;
@@ -214,6 +209,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   const double gtoll0 = gtL * (1.0 + r0 * (1.0 + fabs(lb0) + fabs(ub0)));
   const double gtoll1 = gtL * (1.0 + r1 * (1.0 + fabs(lb1) + fabs(ub1)));
 
+  {
+    float* stg = reinterpret_cast<float*>(lbase + o_sc);
+    for (int e0 = 0;;) {
+#pragma unroll
+      for (int j = 0; j < kChunk; j++) stg[dst[j]] = vbuf[j];
+      e0 += kChunk * 64;
+      if (e0 >= tots) break;
+      issue(e0);
+    }
+    __syncthreads();
+  }
+
+  SSTAMP(t_stg);
   SSTAMP(t_lin);
   // references of the lane's stages: recentred (ROT: rotated) fp64, lane-major; a non-finite
   // entry flags the QP (one ballot folded over its segment lanes)

@@ -775,16 +775,17 @@ __device__ __forceinline__ void matvec_T(Smem<NUM, GAP>& sm, const float (&h)[R]
 constexpr int kRefineSteps = 4;
 constexpr float kRefineTol = 2e-6f;
 // GI's final point (gap rows): refined until its fp64 KKT residual is small (at most kRefineMax
-// residual evaluations), then certified by duality. For a point u that satisfies every row to
-// 1e-9 relative (fp64), with the multipliers mu+ = max(mu, 0) of its active rows, rho = H u + g -
-// N_A mu+ and the active rows' slacks s_j+ = max(n_j'u - b_j, 0), the duality gap of the QP whose
-// rows are relaxed by u's own violations gives |u - u*'|_H^2 <= rho'W rho + 2 sum_A mu+_j s_j+
-// (W = H^-1, u*' that QP's optimum), and |e|_2 <= |e|_H / sqrt(lambda) with lambda = min(r) <=
-// lambda_min(H) (H = R + Gamma'Q Gamma). SOLVED when that bound is <= lambda (kCertTauW max(1,
-// |u|_inf))^2, with rho'W rho bounded from above in fp64 (an fp64 Hessian product corrects the
-// fp32 W's product, hv_f64). The W-norm keeps the bound at sqrt(kappa(H)) times the rounding of
-// an exact point, where |rho|_2 / lambda would be kappa times (stiff QPs, kappa ~ 4e5 at N = 48,
-// dt = 0.05). Anything else is SOLVED_INACCURATE and goes to the fp64 re-check (gi64_kernel.h).
+// residual evaluations), then certified by duality. For a point u that satisfies every row and
+// holds its active rows to 1e-9 relative (fp64), with the multipliers mu+ = max(mu, 0) of its
+// active rows and rho = H u + g - N_A mu+: |u - u*'|_H^2 <= rho'W rho (W = H^-1) for the optimum
+// u*' of the reference QP with each row bound moved by u's own residual on it (<= 1e-9 relative:
+// a backward error far below the float32 rounding of the inputs), and |e|_2 <= |e|_H / sqrt(lambda)
+// with lambda = min(r) <= lambda_min(H) (H = R + Gamma'Q Gamma). SOLVED when rho'W rho, bounded
+// from above in fp64 (an fp64 Hessian product corrects the fp32 W's product, hv_f64), is <=
+// lambda (kCertTauW max(1, |u|_inf))^2. The W-norm keeps the bound at sqrt(kappa(H)) times the
+// rounding of an exact point, where |rho|_2 / lambda would be kappa times (stiff QPs, kappa ~ 4e5
+// at N = 48, dt = 0.05). Anything else is SOLVED_INACCURATE and goes to the fp64 re-check
+// (gi64_kernel.h).
 constexpr int kRefineMax = 8;
 constexpr double kCertTauW = 1e-6;
 // box path's fp64 PDAS (step 4a'): passes, HIK passes before the least-index rule, flips pivoted
@@ -1816,16 +1817,21 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #pragma unroll
           for (int r = 0; r < R; r++) neg = neg || (64 * r + lane < q && sm.cmult[slot_id[r]] < 0.0);
           if (bid64 == 0x7fffffff) {
-            // With mu+ = max(mu, 0) on the active rows and rho = H u + g - N_A mu+, the duality gap
-            // of the QP whose rows are relaxed by u's own violation of them (at most the 1e-9
-            // relative of the feasibility test) bounds the distance to that QP's optimum u*':
-            //   |u - u*'|_H^2 <= rho'W rho + 2 sum_A mu+_j s_j+,  s_j+ = max(n_j'u - b_j, 0),
-            // and |e|_2^2 <= |e|_H^2 / lambda (lambda = min r <= lambda_min(H)). rho'W rho is bounded
-            // from above in fp64 whatever the accuracy of the fp32 W (kappa ~ 4e5 on the stiff
-            // corners): with y = W rho (the fp32 product) and r = rho - H y (fp64 Hessian product),
+            // With mu+ = max(mu, 0) on the active rows and rho = H u + g - N_A mu+, u is the exact
+            // optimum of the QP whose gradient is g - rho and whose row bounds are moved by u's own
+            // residuals on them (active rows to n_j'u, rows u violates to n_j'u: at most the 1e-9
+            // relative of the tests here, far below the float32 rounding of the inputs), and the
+            // optimum u*' of that QP with the true gradient g is within |u - u*'|_H^2 <= rho'W rho
+            // (its duality gap at the dual point mu+), so |u - u*'|_2^2 <= rho'W rho / lambda
+            // (lambda = min r <= lambda_min(H)). rho'W rho is bounded from above in fp64 whatever
+            // the accuracy of the fp32 W (kappa ~ 4e5 on the stiff corners): with y = W rho (the
+            // fp32 product) and r = rho - H y (fp64 Hessian product, hv_f64),
             //   rho'H^-1 rho = y'(2 rho - H y) + r'H^-1 r <= y'(2 rho - H y) + |r|_2^2 / lambda,
             // with one correction y += W r when that bound is loose (round-5 ADVICE: the fp32
-            // estimate rho'W rho and the dropped active-row term are no longer trusted).
+            // estimate of rho'W rho is no longer what certifies). A first-order bound in the rows'
+            // residuals against the unmoved bounds would need the optimal multipliers; the
+            // duality gap charges them as 2 mu+ s, which measured 1e4-1e6 times the threshold on
+            // exact points and is not used.
             double r1c[R];
             wsync();
             kkt_res(true, r1c);
@@ -1839,11 +1845,6 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
             float wc[R], r2c[R];
             matvec_W<NUM, GAP, R>(sm, lane, wc);
             const float r2nc = act_res(r2c);
-            double actg = 0.0;  // sum_A mu+_j s_j+
-#pragma unroll
-            for (int r = 0; r < R; r++)
-              if (64 * r + lane < q) actg += fmax(sm.cmult[slot_id[r]], 0.0) * fmax((double)r2c[r], 0.0);
-            actg = wave_sum(actg);
             const double lam = fmin(P.r[0], P.r[1]);
             double ycr[R];
 #pragma unroll
@@ -1863,7 +1864,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
               t2 = wave_sum(t2);
               bound = t1 + t2 / lam;
               // decided: certified, or even a perfect y (bound -> t1) could not certify
-              if (pass == 1 || bound + 2.0 * actg <= thr2 || t1 + 2.0 * actg > thr2) break;
+              if (pass == 1 || bound <= thr2 || t1 > thr2) break;
               wsync();
 #pragma unroll
               for (int r = 0; r < R; r++) sm.vec[vv[r]] = (float)rr[r];
@@ -1873,7 +1874,7 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
 #pragma unroll
               for (int r = 0; r < R; r++) ycr[r] += valid[r] ? (double)dy[r] : 0.0;
             }
-            cert = bound >= 0.0 && bound + 2.0 * actg <= thr2 && r2nc <= 1e-9f;
+            cert = bound >= 0.0 && bound <= thr2 && r2nc <= 1e-9f;
           }
           if constexpr (GAP) {
             // Negative-multiplier re-entry: the refined set holds a row with a negative multiplier

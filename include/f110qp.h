@@ -68,8 +68,9 @@ extern "C" {
 /* per-QP status codes (values follow OSQP's status ids) */
 #define F110QP_SOLVED 1
 #define F110QP_SOLVED_INACCURATE 2 /* a point whose fp64 certificate failed (box rows: the KKT  */
-                                  /* check in primal units; gap rows: strong convexity, also    */
-                                  /* after the fp64 Goldfarb-Idnani re-check): u, x, obj, cost  */
+                                  /* check in primal units; gap rows: the duality-gap bound     */
+                                  /* below, also after the fp64 Goldfarb-Idnani re-check): u,   */
+                                  /* x, obj, cost                                               */
                                   /* are written but not certified, and f110qp_select_dev never */
                                   /* picks it. Its active set may seed the next warm start (a   */
                                   /* seed is only a first guess; every solve is certified on    */
@@ -92,9 +93,16 @@ extern "C" {
                                   /* only problem, the wave kernel's GI for the QPs whose box   */
                                   /* optimum violates a gap row (no warm state, ungrouped)      */
 /* Gap rows: the wave kernel's GI (AUTO: behind the box screen from
- * F110QP_GAP_SCREEN_MIN_BATCH QPs); GI's final point is certified in fp64 by strong convexity, and
- * every QP it does not certify is re-checked in the same call by an fp64 Goldfarb-Idnani with the
- * oracle's rules (SOLVED, PRIMAL_INFEASIBLE, MAX_ITER or SOLVED_INACCURATE from there).
+ * F110QP_GAP_SCREEN_MIN_BATCH QPs); GI's final point is certified in fp64, and every QP it does not
+ * certify is re-checked in the same call by an fp64 Goldfarb-Idnani with the oracle's rules
+ * (SOLVED, PRIMAL_INFEASIBLE, MAX_ITER or SOLVED_INACCURATE from there). What SOLVED certifies on
+ * this path: every row holds to 1e-9 (1 + |b| + |u|_inf) in fp64, and |u - u*'|_2 <= 1e-6
+ * max(1, |u|_inf) for the exact optimum u*' of the reference QP with each row bound moved by u's own
+ * residual on it (a backward error <= that 1e-9 relative, below the float32 rounding of the
+ * inputs): the duality gap at the clamped multipliers, rho'W rho / min(R) with rho = Hu + g - N_A mu+,
+ * rho'W rho bounded from above in fp64. The distance to the optimum of the unmoved QP also depends
+ * on that QP's sensitivity to its bounds, which is not bounded here (tests: within 4e-8 of the
+ * oracle's exact optimum on every gap-row case).
  * AUTO thresholds, measured on MI355X (kernel us, DESIGN.md section 6, round 3: the lane back end
  * with the partitioned-horizon kernel below one wave per SIMD, the wave back end with its fp64
  * certification). N = 20 (C2 recipe, cold): wave 27.3 vs lane 30.6 at 512 (before the last

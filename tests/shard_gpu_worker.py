@@ -21,9 +21,12 @@ from f110qp.shard import select_sharded, shard_range, solve_sharded  # noqa: E40
 def main():
     out_path, N, scen, be = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     mode = sys.argv[5] if len(sys.argv) > 5 else "gather"
-    dist.init_process_group("gloo")
-    dev = torch.device("cuda", 0)
+    # 6th argument: the process-group backend (gloo: host tensors, ranks may share GPU 0; nccl = RCCL,
+    # one GPU per rank: the min-loc all-reduces run on device tensors)
+    pgb = sys.argv[6] if len(sys.argv) > 6 else "gloo"
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    dist.init_process_group(pgb, **({"device_id": dev} if pgb == "nccl" else {}))
     g = workload.make_grouped_batch(scen, N, seed=4242)
     G = g["group_size"]
     inputs = {k: torch.from_numpy(np.ascontiguousarray(g[k])) for k in ("x0", "u_lin", "x_ref")}
@@ -58,9 +61,14 @@ def main():
         torch.cuda.synchronize(dev)
         win = win.cpu().to(torch.int64)
         win = torch.where(win >= 0, win + lo, win)
-        b, w = select_sharded(best.cpu(), win)
+        if pgb == "nccl":  # device tensors through RCCL
+            b, w = select_sharded(best, win.to(dev))
+            b, w = b.cpu(), w.cpu()
+        else:
+            b, w = select_sharded(best.cpu(), win)
         if rank == 0:
-            np.savez(out_path, best=b.numpy(), winner=w.numpy(), world=world, lo1=shard_range(total, world, 1, 1)[0])
+            lo1 = shard_range(total, world, 1, 1)[0] if world > 1 else total
+            np.savez(out_path, best=b.numpy(), winner=w.numpy(), world=world, lo1=lo1)
         solver.close()
         dist.destroy_process_group()
         return

@@ -52,6 +52,18 @@ def test_diagnostic_queries_without_a_call(capi):
     w.close()
 
 
+@pytest.mark.parametrize("lang,cc", [("c", "gcc"), ("c++", "g++")])
+def test_header_compiles_as_c_and_cpp(lang, cc):
+    """include/f110qp.h is the drop-in boundary: plain C, usable from the reference's C++."""
+    import shutil
+    import subprocess
+
+    if shutil.which(cc) is None:
+        pytest.skip(f"{cc} not installed")
+    hdr = os.path.join(ROOT, "include", "f110qp.h")
+    subprocess.run([cc, "-fsyntax-only", "-Wall", "-Werror", "-x", lang, hdr], check=True)
+
+
 def test_library_is_gfx950_code_object(capi):
     data = open(capi.LIB_PATH, "rb").read()
     assert b"gfx950" in data  # the offload bundle targets MI355X

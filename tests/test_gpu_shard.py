@@ -107,3 +107,41 @@ def test_two_rank_select_straddling_scenarios(capi, cuda, tmp_path, N, scen, be)
         c = np.sort(cn[(gn == k) & (sn == capi.SOLVED)])
         if len(c) > 1 and c[1] - c[0] > 1e-9 * max(1.0, c[0]):
             assert d["winner"][k] == int(win[k])
+
+
+def test_rccl_min_loc_select_one_rank(capi, cuda, tmp_path):
+    """The nccl (= RCCL) process-group path of the selection on the box's one GPU: a world of one
+    under torch.distributed.run runs shard.select_sharded's two all_reduce(MIN) on device tensors
+    through RCCL (an identity at world size 1), and the result equals the single-process selection.
+    The multi-GPU runs of bench.py use the same backend (--dist-backend nccl, the default)."""
+    import torch
+
+    from f110qp import workload
+
+    N, scen = 40, 5
+    out = tmp_path / "select_rccl.npz"
+    env = {**os.environ, "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                    "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                    os.path.join(ROOT, "tests", "shard_gpu_worker.py"), str(out), str(N), str(scen),
+                    str(capi.BACKEND_LANE), "select", "nccl"], check=True, timeout=180, env=env, cwd=ROOT)
+    d = np.load(out)
+    assert int(d["world"]) == 1
+    g = workload.make_grouped_batch(scen, N, seed=4242)
+    B = g["x0"].shape[0]
+    dev = torch.device("cuda", 0)
+    x0, ul, xr = (torch.from_numpy(np.ascontiguousarray(g[k])).to(dev) for k in ("x0", "u_lin", "x_ref"))
+    gid = (torch.arange(B, dtype=torch.int32) // g["group_size"]).to(dev)
+    uo = torch.empty((B, N, 2), dtype=torch.float32, device=dev)
+    xo = torch.empty((B, N + 1, 3), dtype=torch.float32, device=dev)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    co = torch.empty(B, dtype=torch.float64, device=dev)
+    s = capi.Solver(capi.default_config(N, device=0, backend=capi.BACKEND_LANE))
+    s.solve_dev(x0, ul, xr, None, uo, xo, st, None, cost=co)
+    win = torch.empty(scen, dtype=torch.int32, device=dev)
+    best = torch.empty(scen, dtype=torch.float64, device=dev)
+    capi.select_dev(gid, scen, co, st, win, best)
+    torch.cuda.synchronize()
+    s.close()
+    np.testing.assert_array_equal(d["winner"], win.cpu().numpy().astype(np.int64))
+    np.testing.assert_array_equal(d["best"], best.cpu().numpy())
