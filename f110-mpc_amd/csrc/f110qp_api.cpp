@@ -108,6 +108,7 @@ struct f110qp_ctx {
   int lane_dref = 1;         // lane fp64 references in LDS when they fit (LaneWork::dref)
   int lane_seg = 0;          // lane horizon segments per QP (LaneWork::seg: 0 auto, 1 off, 2/4/8)
   int lane_seg32 = 0;        // segmented kernel: force fp32 references + scratch (LaneWork::seg32)
+  int lane_twin = 1;         // segmented kernel: twin PDAS starts where they fit (LaneWork::twin)
   int gap_screen = -1;      // gap rows, AUTO: box screen on the lane kernel (-1 by batch, 0 off, 1 on)
   int recheck_all = 0;      // gap rows: every QP of a call through the fp64 re-check alone (test build)
   hipStream_t stream = nullptr;
@@ -146,6 +147,8 @@ static void test_hooks(f110qp_ctx* c) {
   if (env_int("F110QP_LANE_SEG", 0, 8, &v) && (v == 0 || v == 1 || v == 2 || v == 4 || v == 8)) c->lane_seg = v;
   // 1: the segmented kernel's float references and scratch
   if (env_int("F110QP_LANE_SEG_F32", 0, 1, &v)) c->lane_seg32 = v;
+  // 0: one PDAS start per QP in the segmented kernel (the twin start off)
+  if (env_int("F110QP_LANE_TWIN", 0, 1, &v)) c->lane_twin = v;
   // gap rows: the box screen on (1) / off (0) at every batch size
   if (env_int("F110QP_GAP_SCREEN", 0, 1, &v)) c->gap_screen = v;
   // wave GI: 0 picks gap and box candidates by one ranking
@@ -329,6 +332,7 @@ static int lane_work(f110qp_ctx* c, int batch, hipStream_t s, int* backend, f110
   lw->dref = c->lane_dref;
   lw->seg = c->lane_seg;
   lw->seg32 = c->lane_seg32;
+  lw->twin = c->lane_twin;
   *backend = resolve_backend(c, batch, grouped) == F110QP_BACKEND_LANE ? f110qp::BACKEND_LANE
                                                                       : f110qp::BACKEND_WAVE;
   hipError_t e;
@@ -535,6 +539,7 @@ int f110qp_backend_info(f110qp_ctx* c, int batch, int grouped, int* backend, int
   if (backend) *backend = be;
   if (qps_per_wave) *qps_per_wave = lane ? (segs > 1 ? 64 / segs : f110qp::lane_qps_per_wave(batch, lw.qpw)) : 1;
   lw.seg32 = c->lane_seg32;
+  lw.twin = c->lane_twin;
   if (scratch)
     *scratch = !lane ? 0 : segs > 1 ? f110qp::lane_seg_scratch(c->kp, batch, segs, lw)
                                     : f110qp::lane_scratch_mode(c->kp, batch, lw);
@@ -553,6 +558,22 @@ int f110qp_lane_segments(f110qp_ctx* c, int batch, int* segments) {
   lw.seg = c->lane_seg;
   if (be != F110QP_BACKEND_LANE) *segments = 1;
   else *segments = f110qp::lane_segments(c->kp, batch, lw);
+  return F110QP_OK;
+}
+
+int f110qp_lane_starts(f110qp_ctx* c, int batch, int* starts) {
+  if (!c || !starts) return fail(F110QP_ERR_INVALID, "ctx / starts is NULL");
+  if (batch < 1) return fail(F110QP_ERR_INVALID, "batch must be >= 1");
+  int segs = 1;
+  const int rc = f110qp_lane_segments(c, batch, &segs);
+  if (rc) return rc;
+  f110qp::LaneWork lw;
+  lw.mode = c->lane_mode;
+  lw.qpw = c->lane_qpw;
+  lw.seg = c->lane_seg;
+  lw.seg32 = c->lane_seg32;
+  lw.twin = c->lane_twin;
+  *starts = segs > 1 ? f110qp::lane_seg_starts(c->kp, batch, segs, lw) : 1;
   return F110QP_OK;
 }
 

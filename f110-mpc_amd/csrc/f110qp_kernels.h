@@ -95,6 +95,7 @@ struct LaneWork {
   int dref = 1;   // 1: fp64 references in LDS when the resident waves fit (DREF); 0: float
   int seg = 0;    // horizon segments per QP (lane_seg_kernel.h): 0 auto, 1 off, 2 / 4 / 8 forced
   int seg32 = 0;  // segmented kernel: 1 forces float references and Riccati scratch in LDS
+  int twin = 1;   // segmented kernel: two PDAS starts per QP where the grid leaves SIMDs idle
   int* hand = nullptr;  // gap rows: counts + per-QP lists (HandLayout, kHandInts(B) ints)
   int screen = 0;       // gap rows: box solve on the lane kernel first, GI only for the QPs whose
                         // box optimum violates a gap row (f110qp_kernels.hip)
@@ -129,6 +130,8 @@ int lane_scratch_mode(const KParams& P, int B, const LaneWork& lw);
 int lane_segments(const KParams& P, int B, const LaneWork& lw);
 // scratch of the segmented kernel at S segments: 1 LDS fp64, 2 LDS fp32 (lane_seg_kernel.h)
 int lane_seg_scratch(const KParams& P, int B, int S, const LaneWork& lw);
+// PDAS starts per QP of the segmented kernel at S segments: 2 with the twin start (lane_seg_kernel.h)
+int lane_seg_starts(const KParams& P, int B, int S, const LaneWork& lw);
 
 // fp64 re-check of the gap-row QPs the wave kernel did not report SOLVED (its certificate
 // failed, or GI ended infeasible / at its cap): the fp64 Goldfarb-Idnani of gi64_kernel.h over

@@ -32,6 +32,9 @@ F110QP_SEG_INST_ALL(true)
 #undef F110QP_SEG_INST
 
 #if defined(F110QP_SEG_ALL) || F110QP_SEG_SCR == 0
-int lane_seg_scratch(const KParams& P, int B, int S, const LaneWork& lw) { return seg_scratch_mode(P, B, S, lw); }
+int lane_seg_scratch(const KParams& P, int B, int S, const LaneWork& lw) {
+  return seg_scratch_mode(P, seg_twin(P, B, S, lw) ? 2 * B : B, S, lw);
+}
+int lane_seg_starts(const KParams& P, int B, int S, const LaneWork& lw) { return seg_twin(P, B, S, lw) ? 2 : 1; }
 #endif
 }  // namespace f110qp

@@ -94,24 +94,34 @@ __device__ __forceinline__ double seg_shfl(double v, int src) {
 // neutral (tools/ab_seg_variant.sh)
 #define F110QP_SEG_WPE 2
 #endif
-template <int S, bool ROT, bool FST, typename ST = double, bool SCR = false>
+template <int S, bool ROT, bool FST, typename ST = double, bool SCR = false, bool TWIN = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_WPE, F110QP_SEG_WPE))) void lane_seg_kernel(
     const KParams P, const int B, const float* __restrict__ x0g, const float* __restrict__ ulg,
     const float* __restrict__ xrg, float* __restrict__ uout, float* __restrict__ xout,
     int* __restrict__ status_out, int* __restrict__ iters_out, const WarmState ws, const int kmax,
     const ObjOut oo) {
+  constexpr int twin = TWIN ? 1 : 0;
   constexpr int L = 64 / S;  // QPs per wave
   constexpr int NV = FST ? 14 : 11;  // scratch doubles per stage: K 6, k 2, then F 6 or S^-1 3
   extern __shared__ __attribute__((aligned(16))) double seg_smem[];
   const int lane = threadIdx.x;
   const int sl = lane & (L - 1);
   const int seg = lane / L;
-  const int b0 = blockIdx.x * L;
-  const int nq = (B - b0) < L ? (B - b0) : L;
-  const int slot = sl < nq ? sl : 0;  // a missing QP's lanes duplicate QP 0 of the wave
-  const bool owner = sl < nq;          // stores the outputs of its segment's stages
-  const bool qowner = owner && seg == 0;
-  const int b = b0 + slot;
+  // twin = 1: every QP is solved from two PDAS starts at once, adjacent slots 2b (cold) and 2b + 1
+  // (the speed bound nearest u_des active on the first half of the horizon); the QP is done when
+  // either start has converged, and the converged one (the cold one on a tie) writes the outputs.
+  // Both end at the same exact optimum; the pass count is the smaller one (launch_lane_seg_t)
+  const int b0 = blockIdx.x * L;                 // first (virtual) QP of the wave
+  const int VB = B << twin;
+  const int nq = (VB - b0) < L ? (VB - b0) : L;
+  // a missing QP's lanes duplicate QP 0 of the wave (twin: the start of the same parity, so that a
+  // duplicate's sibling lane is a duplicate of its sibling start)
+  const int slot = sl < nq ? sl : (sl & twin);
+  const bool owner0 = sl < nq;         // stores the outputs of its segment's stages ...
+  const bool qowner0 = owner0 && seg == 0;
+  const int vq = b0 + slot;
+  const bool var = (vq & twin) != 0;   // ... if its start is the one that converged (owner below)
+  const int b = vq >> twin;
   const int N = P.N;
   // segments of q or q + 1 stages (the first N mod S ones longer); LDS rows for the longest
   const int q = N / S, rem = N - q * S;
@@ -141,39 +151,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   // stg[c L + q]. (q, c) advance by 64 elements per step without a division, every load reads a
   // valid address (clamped) and every store lands (past the staged rows for e >= tot), so the
   // loop has no EXEC-masked region: ~11 instructions per element instead of ~50 (ISA).
-  // Chunk 0's loads are issued first and the linearisation below runs while they are in flight
-  // (it needs only the per-QP scalars above); then the chunks go to LDS.
-  const int n3s = 3 * N, S3 = 3 * P.xr_stride, tots = nq * n3s;
-  const float* const srcs = xrg + (size_t)b0 * S3;
-  const int dqs = 64 / n3s, dcs = 64 - dqs * n3s;
-  int sq = lane / n3s, scol = lane - (lane / n3s) * n3s;
-  const int junk = n3s * L + lane;                  // inside the scratch rows, never read
-  const int last_off = (nq - 1) * S3 + (n3s - 1);  // a valid element for the clamped loads
-  constexpr int kChunk = 16;  // C5 and the C4 shard stage 960 floats per wave: one round trip
-  float vbuf[kChunk];
-  int dst[kChunk];
-  auto issue = [&](int e0) __attribute__((always_inline)) {
+  // (Issuing chunk 0 first and the linearisation under its loads measured no gain: C2 23.4 against
+  // 23.1 us, C5 30.9 against 30.4, same box.) Twin starts: row q of the wave is QP (b0 + q) >> 1.
+  {
+    float* stg = reinterpret_cast<float*>(lbase + o_sc);
+    const int n3 = 3 * N, S3 = 3 * P.xr_stride, tot = nq * n3;
+    const int rb0 = b0 >> twin;
+    const float* src = xrg + (size_t)rb0 * S3;
+    const int dq = 64 / n3, dc = 64 - dq * n3;
+    int q = lane / n3, c = lane - (lane / n3) * n3;
+    const int junk = n3 * L + lane;                  // inside the scratch rows, never read
+    const int last_off = (((b0 + nq - 1) >> twin) - rb0) * S3 + (n3 - 1);  // a valid element
+    constexpr int kChunk = 16;  // C5 and the C4 shard stage 960 floats per wave: one round trip
+    for (int e0 = 0; e0 < tot; e0 += kChunk * 64) {
+      float vbuf[kChunk];
+      int dst[kChunk];
 #pragma unroll
-    for (int j = 0; j < kChunk; j++) {
-      const bool in = e0 + j * 64 + lane < tots;
-      dst[j] = in ? scol * L + sq : junk;
-      vbuf[j] = srcs[in ? sq * S3 + scol : last_off];
-      sq += dqs;
-      scol += dcs;
-      const bool wrap = scol >= n3s;
-      scol -= wrap ? n3s : 0;
-      sq += wrap ? 1 : 0;
+      for (int j = 0; j < kChunk; j++) {
+        const bool in = e0 + j * 64 + lane < tot;
+        dst[j] = in ? c * L + q : junk;
+        vbuf[j] = src[in ? (((b0 & twin) + q) >> twin) * S3 + c : last_off];
+        q += dq;
+        c += dc;
+        const bool wrap = c >= n3;
+        c -= wrap ? n3 : 0;
+        q += wrap ? 1 : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < kChunk; j++) stg[dst[j]] = vbuf[j];
     }
-  };
-  issue(0);
-  // the warm-start key, when this call moves warm traffic (its round trip, like the staging
-  // loads', overlaps the linearisation below)
+    __syncthreads();
+  }
+  // the warm-start key, when this call moves warm traffic (its round trip overlaps the staging)
   const bool wt = warm_traffic(ws, wlast);
   unsigned key0 = 0u, key1 = 0u, key2 = 0u, key3 = 0u;
   if (wt) {
     const uint4 k4 = *reinterpret_cast<const uint4*>(ws.key + 4 * (size_t)b);
     key0 = k4.x; key1 = k4.y; key2 = k4.z; key3 = k4.w;
   }
+
+  SSTAMP(t_stg);
   // ---- per-lane QP data (Model::Linearize, model.cpp:30-59), as lane_kernel.h ----
   const double X0 = (double)fX0, Y0 = (double)fY0;
   const double th0 = (double)fTH0;
@@ -209,19 +226,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   const double gtoll0 = gtL * (1.0 + r0 * (1.0 + fabs(lb0) + fabs(ub0)));
   const double gtoll1 = gtL * (1.0 + r1 * (1.0 + fabs(lb1) + fabs(ub1)));
 
-  {
-    float* stg = reinterpret_cast<float*>(lbase + o_sc);
-    for (int e0 = 0;;) {
-#pragma unroll
-      for (int j = 0; j < kChunk; j++) stg[dst[j]] = vbuf[j];
-      e0 += kChunk * 64;
-      if (e0 >= tots) break;
-      issue(e0);
-    }
-    __syncthreads();
-  }
-
-  SSTAMP(t_stg);
   SSTAMP(t_lin);
   // references of the lane's stages: recentred (ROT: rotated) fp64, lane-major; a non-finite
   // entry flags the QP (one ballot folded over its segment lanes)
@@ -259,7 +263,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
 #endif
     if (ws.hit_call && __ballot(hit) != 0ull && lane == 0) *ws.hit_call = ws.call;
     if (ws.stats && wt) {  // f110qp_warm_hits: traffic calls (wave 0), hits (one lane per QP)
-      const unsigned nh = (unsigned)__popcll(__ballot(hit && qowner));
+      const unsigned nh = (unsigned)__popcll(__ballot(hit && qowner0 && !var));
       if (lane == 0 && nh) atomicAdd(ws.stats + 1, nh);
       if (lane == 0 && blockIdx.x == 0) atomicAdd(ws.stats, 1u);
     }
@@ -280,6 +284,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     for (int t = 0; t < m; t++) {  // per input: 1 lower, 2 upper, 0 free; the lower bound wins
       const unsigned l2 = (unsigned)(lw >> (2 * t)) & 3u, h2 = (unsigned)(hw >> (2 * t)) & 3u & ~l2;
       ap[t * 64] = (int)((l2 & 1u) | ((h2 & 1u) << 1) | ((l2 & 2u) << 1) | ((h2 & 2u) << 2));
+    }
+    // the twin start: the speed bound u_des sits on, active on the first half of the horizon (on
+    // the C2 / C5 workloads the optimum holds the speed on its upper bound over a prefix of the
+    // horizon that cold PDAS finds a few stages per pass: numpy model of the kernel's PDAS, the
+    // slowest QP's passes 4-5 -> 3-4 over eight C2 batches and six C5 ticks; launch_lane_seg_t
+    // enables it only when u_des is on a speed bound)
+    if (var && !hit) {
+      const int sv = ud0 >= ub0 ? 2 : (ud0 <= lb0 ? 1 : 0);
+      for (int t = 0; t < m; t++)
+        if (2 * (s0 + t) < N) ap[t * 64] = sv;
     }
   }
 
@@ -303,7 +317,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   t_setup = __builtin_amdgcn_s_memtime() - t_start;
 #endif
   for (int pass = 0; pass < max_pass; pass++) {
-    if (__ballot(!done) == 0ull) break;
+    // a QP is finished when one of its starts is (twin: the sibling start is the next lane). The
+    // shuffle runs on every lane: under a short-circuit || the done lanes are off in EXEC, and a
+    // permute reads nothing from an inactive source lane
+    if constexpr (TWIN) {
+      const int sib = __shfl_xor((int)done, 1, 64);
+      if (__ballot(!(done || sib != 0)) == 0ull) break;
+    } else {
+      if (__ballot(!done) == 0ull) break;
+    }
     const bool single = pass >= kmax;
 #ifdef F110QP_STAMPS
     npass++;
@@ -649,6 +671,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   }
 
   SSTAMP(t_out);
+  // the start whose outputs stand: the one that converged first (a converged start keeps its
+  // iteration count while its wave sweeps on), the cold one on a tie or when neither converged
+  bool owner = owner0, qowner = qowner0;
+  if constexpr (TWIN) {
+    const bool sdone = __shfl_xor((int)done, 1, 64) != 0;
+    const int sibit = __shfl_xor(iters, 1, 64);
+    const bool win = var ? (done && (!sdone || iters < sibit)) : (done ? (!sdone || iters <= sibit) : !sdone);
+    owner = owner0 && win;
+    qowner = qowner0 && win;
+  }
   // ---- output sweep: u* = K x + k from the final gains, x* by the fp64 rollout ----
   const bool solved = done && !bad;
   const float nanv = __int_as_float(0x7fc00000);
@@ -796,13 +828,28 @@ inline int seg_scratch_mode(const KParams& P, int B, int S, const LaneWork& lw) 
   return f64 ? 1 : (f32 ? 2 : 0);
 }
 
+// Twin starts (lane_seg_kernel<..., TWIN = true>): each QP solved from the cold start and from the
+// speed bound u_des sits on held over the first half of the horizon, in adjacent slots of one wave.
+// Taken when u_des is on a speed bound (the shipped params.yaml:42,46: des_vel = umax) and the
+// doubled grid is still at most one wave per CU: C2 (1,024 QPs, 128 waves) 26.4 -> 23.4 us, but C5
+// (4,096, 512 waves, two per CU) 28.8 -> 30.9 although its slowest tick's passes went 5 -> 4 (same
+// box). lw.twin = 0 (test build, F110QP_LANE_TWIN=0) turns it off.
+constexpr long kTwinMaxWaves = 256;
+inline bool seg_twin(const KParams& P, int B, int S, const LaneWork& lw) {
+  if (!lw.twin || !(P.udes[0] >= (double)P.umax[0] || P.udes[0] <= (double)P.umin[0])) return false;
+  const long waves2 = (2L * B * S + 63) / 64;
+  return waves2 <= kTwinMaxWaves && seg_scratch_mode(P, 2 * B, S, lw) == 1 && lw.dref &&
+         seg_lds_bytes(P.N, S, true) <= 160 * 1024;  // the lam-gain (FST) kernel, one wave per CU
+}
+
 template <int S, bool ROT, bool SCR>
 hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const float* ul, const float* xr,
                              float* uo, float* xo, int* st, int* its, const WarmState& ws,
                              const LaneWork& lw, const ObjOut& oo, hipStream_t s) {
   constexpr int L = 64 / S;
-  const int waves = (B + L - 1) / L;
-  const int mode = seg_scratch_mode(P, B, S, lw);
+  const int twin = seg_twin(P, B, S, lw) ? 1 : 0;  // (one wave per CU at most: FST fits)
+  const int waves = ((B << twin) + L - 1) / L;
+  const int mode = seg_scratch_mode(P, B << twin, S, lw);
   // the lam-gains stored (FST, no refresh sweep: measured C5 30.5 -> see DESIGN.md 2b') when the
   // resident waves' LDS holds 14 doubles per stage, else the refresh sweep (11); lw.dref = 0
   // forces the refresh (test hook, F110QP_LANE_DREF=0)
@@ -818,6 +865,7 @@ hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const flo
                        lw.kmax, oo);
     return hipGetLastError();
   };
+  if (twin) return go(&lane_seg_kernel<S, ROT, true, double, SCR, true>, seg_lds_bytes(P.N, S, true));
   if (mode == 2) return go(&lane_seg_kernel<S, ROT, false, float, SCR>, seg_lds_bytes(P.N, S, false, true));
   return fst ? go(&lane_seg_kernel<S, ROT, true, double, SCR>, seg_lds_bytes(P.N, S, true))
              : go(&lane_seg_kernel<S, ROT, false, double, SCR>, seg_lds_bytes(P.N, S, false));

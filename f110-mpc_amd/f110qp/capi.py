@@ -90,6 +90,7 @@ EXPORTED = (
     "f110qp_lane_segments",
     "f110qp_gap_screen",
     "f110qp_last_recheck_count",
+    "f110qp_lane_starts",
     "f110qp_warm_hits",
     "f110qp_test_build",
 )
@@ -164,6 +165,7 @@ def load(test: bool = False):
     L.f110qp_lane_segments.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.f110qp_gap_screen.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.f110qp_last_recheck_count.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    L.f110qp_lane_starts.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.f110qp_warm_hits.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.f110qp_test_build.restype = C.c_int
     L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
@@ -293,6 +295,13 @@ class Solver:
         2 / 4 / 8 when the lane back end runs the partitioned Riccati (lane_seg_kernel.h)."""
         v = C.c_int()
         self._chk(self.lib.f110qp_lane_segments(self._h, int(batch), C.byref(v)), "f110qp_lane_segments")
+        return v.value
+
+    def lane_starts(self, batch: int) -> int:
+        """PDAS starts per QP of a solve call of `batch` QPs (f110qp_lane_starts): 2 with the
+        partitioned-horizon kernel's twin start, else 1."""
+        v = C.c_int()
+        self._chk(self.lib.f110qp_lane_starts(self._h, int(batch), C.byref(v)), "f110qp_lane_starts")
         return v.value
 
     def last_recheck_count(self) -> int:

@@ -259,6 +259,13 @@ int f110qp_backend_info(f110qp_ctx* ctx, int batch, int grouped, int* backend, i
  * The result is the exact optimum either way. */
 int f110qp_lane_segments(f110qp_ctx* ctx, int batch, int* segments);
 
+/* PDAS starts per QP of that launch: 2 when the partitioned-horizon kernel solves each QP from two
+ * starts at once (the cold one and the speed bound u_des sits on held over the first half of the
+ * horizon; taken when u_des is on a speed bound and the doubled grid still leaves no SIMD with
+ * two waves), else 1. The first start to converge gives the answer: the same exact optimum, in the
+ * smaller of the two pass counts (DESIGN.md 2b'). */
+int f110qp_lane_starts(f110qp_ctx* ctx, int batch, int* starts);
+
 /* on = 1 when a gap-row call of `batch` QPs takes the box screen (F110QP_GAP_SCREEN_MIN_BATCH):
  * the lane back end solves the box-only problem, the wave kernel's GI only the QPs whose box
  * optimum does not keep every gap row (an ungrouped solve call; replaces nothing in the reference:

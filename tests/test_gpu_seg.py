@@ -61,6 +61,7 @@ def test_segments_single_flip(oracle, capi, knob, monkeypatch, kmax, S, N):
     over its segment lanes; the other segments undo theirs): exact results, more passes."""
     knob("F110QP_LANE_SEG", S)
     knob("F110QP_LANE_KMAX", kmax)
+    knob("F110QP_LANE_TWIN", "0")  # one start: the iterates are the sequential kernel's
     w = workload.make_batch(1200, N, seed=992 + N, heading="true", lateral=1.5, steer_range=1.0)
     u, x, st, it = check(oracle, capi, N, w, backend=capi.BACKEND_LANE)
     knob("F110QP_LANE_SEG", "1")
@@ -83,6 +84,7 @@ def test_segments_agree_with_sequential(capi, knob, monkeypatch, S):
     status, solutions within 1e-7."""
     N, B = 40, 2048
     w = workload.make_batch(B, N, seed=2222, heading="true", lateral=1.2, steer_range=0.8)
+    knob("F110QP_LANE_TWIN", "0")  # one start: the iterates are the sequential kernel's
     out = {}
     for seg in ("1", S):
         knob("F110QP_LANE_SEG", seg)
@@ -252,3 +254,32 @@ def test_c4_16384_per_gpu_auto(oracle, capi):
     ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][idx], w["u_lin"][idx], w["x_ref"][idx])
     assert (sr == oracle.SOLVED).all()
     assert rel_err(u[idx], ur).max() <= 2e-6 and rel_err(x[idx], xr).max() <= 2e-6
+
+
+@pytest.mark.parametrize("N,B", [(20, 1024), (20, 2048), (20, 4096), (30, 1000), (40, 512), (20, 1)])
+def test_twin_starts_match_one_start(oracle, capi, knob, N, B):
+    """Twin starts (f110qp_lane_starts = 2: every QP also solved from the speed bound u_des sits on
+    held over the first half of the horizon, the first start to converge answers): the same statuses
+    and optimum as one start (F110QP_LANE_TWIN=0), never more passes, fewer on the QPs whose cold PDAS
+    walks that prefix a few stages per pass; the objective outputs from the winning start. The pass
+    counts equal the numpy model's min over the two starts (DESIGN.md 2b')."""
+    w = workload.make_batch(B, N, seed=8100 + N + B, heading="true", lateral=1.0, steer_range=0.6)
+    out = {}
+    for twin in ("1", "0"):
+        knob("F110QP_LANE_TWIN", twin)
+        s = _lane(capi, N)
+        out[twin] = (s.lane_starts(B), s.lane_segments(B)) + tuple(s.solve(w["x0"], w["u_lin"], w["x_ref"],
+                                                                           objective=True))
+        s.close()
+    (n2, S2, u2, x2, s2, it2, ob2, co2), (n1, S1, u1, x1, s1, it1, ob1, co1) = out["1"], out["0"]
+    # twin where the doubled grid is at most one wave per CU (256 waves; lane_seg_kernel.h seg_twin)
+    assert n1 == 1 and S2 == S1 and (n2 == 2) == (S1 > 1 and 2 * B * S1 <= 256 * 64), (n1, n2, S1, S2)
+    np.testing.assert_array_equal(s2, s1)
+    assert (s2 == capi.SOLVED).all()
+    assert rel_err(u2, u1.astype(np.float64)).max() <= 1e-6 and rel_err(x2, x1.astype(np.float64)).max() <= 1e-6
+    np.testing.assert_allclose(ob2, ob1, rtol=1e-9, atol=1e-9 * np.abs(ob1).max())
+    assert (it2 <= it1).all()
+    if n2 == 2 and B >= 1024:
+        assert it2.max() < it1.max() or it2.mean() < it1.mean()
+    ur, xr, sr = oracle.solve_batch(oracle.params(N), w["x0"][::7], w["u_lin"][::7], w["x_ref"][::7])
+    assert rel_err(u2[::7], ur).max() <= TOL and rel_err(x2[::7], xr).max() <= TOL

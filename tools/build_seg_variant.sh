@@ -8,6 +8,6 @@ d=build_var/$name; mkdir -p $d lib_var/$name
 cp csrc/lane_seg_inst.hip csrc/f110qp_kernels.h $d/
 cp $src/lane_seg_kernel.h $d/
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../include -I$d $* -c $d/lane_seg_inst.hip -o $d/lane_seg_inst.o
-others=$(ls build_obj/*.o | grep -v "build_obj/lane_seg_inst.o")
+others=$(ls build_obj/*.o | grep -v "build_obj/lane_seg_inst.o" | grep -v "build_obj/f110qp_api_test.o")
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib_var/$name/libf110qp.so $others $d/lane_seg_inst.o
 echo built lib_var/$name/libf110qp.so
