@@ -502,6 +502,7 @@ def main():
     eff, lane_qpw, lane_scr = solver.backend_info(Bper, grouped)
     be_name = "lane" if eff == capi.BACKEND_LANE else "wave"
     lane_seg = solver.lane_segments(Bper) if be_name == "lane" else 1
+    lane_starts = solver.lane_starts(Bper) if be_name == "lane" else 1
     if be_name == "lane":
         dtype = "fp64" if lane_scr in (1, 3) else "fp64 (fp32 Riccati-gain scratch in " + (
             "LDS)" if lane_scr == 2 else "HBM)")
@@ -674,7 +675,7 @@ def main():
                                 "clear" if gap else "lane-per-QP (Riccati/PDAS fp64)"}[be_name]
                        + (" grouped: one W = H^-1 per scenario" if grouped and be_name == "wave" else ""),
             **({"lane_qps_per_wave": lane_qpw, "lane_scratch": capi.SCRATCH_NAMES[lane_scr],
-                "lane_segments": lane_seg}
+                "lane_segments": lane_seg, "lane_pdas_starts": lane_starts}
                if be_name == "lane" else {}),
             "parallelism": f"independent QP shards x{world} (no collective)"
                            + (f", scenario-aligned ({GROUP}) split of one global batch" if strong else ""),
@@ -714,8 +715,10 @@ def main():
             **({"segmentation_overhead": seg_overhead} if seg_overhead else {}),
             "note": ("lane kernel: fp64 VALU-issue and scratch-latency bound (Riccati sweeps, 64 QPs per "
                      "wave); traffic = PMC HBM bytes incl. the Riccati scratch" if be_name == "lane" and lane_seg == 1 else
-                     f"partitioned-horizon lane kernel: one QP per {lane_seg} lanes, latency-bound by the slowest "
-                     "QP's PDAS passes x (N/S stages + S-1 segment steps); scratch in LDS, HBM = inputs/outputs"
+                     f"partitioned-horizon lane kernel: one QP per {lane_seg} lanes"
+                     + (" x 2 PDAS starts (twin: the first to converge answers)" if lane_starts == 2 else "")
+                     + ", latency-bound by the slowest QP's PDAS passes x (N/S stages + S-1 segment steps); "
+                     "scratch in LDS, HBM = inputs/outputs"
                      if be_name == "lane" else
                      "wave kernel: latency-bound (serial active-set chain per wave); neither HBM nor FP32 "
                      "peak binds"),

@@ -273,11 +273,12 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
   hipError_t e;
   // keys (16 B per QP), then the lane back ends' last-hit call (warm_traffic) and the cumulative
   // traffic-call and hit counters (f110qp_warm_hits)
-  if ((e = c->wW.ensure(B * nu * nu * 4)) || (e = c->wkey.ensure(B * 16 + 16)) ||
+  const size_t wbytes = B * 16 + 16 + 8 * (B + 1);  // keys, last-hit call, per-wave counters
+  if ((e = c->wW.ensure(B * nu * nu * 4)) || (e = c->wkey.ensure(wbytes)) ||
       (e = c->wact.ensure(B * 16 * rows)))
     return hip_fail(e, "hipMalloc warm-start state");
   if (c->warm_batch != batch) {
-    if ((e = hipMemsetAsync(c->wkey.p, 0, B * 16 + 16, s)) || (e = hipMemsetAsync(c->wact.p, 0, B * 16 * rows, s)))
+    if ((e = hipMemsetAsync(c->wkey.p, 0, wbytes, s)) || (e = hipMemsetAsync(c->wact.p, 0, B * 16 * rows, s)))
       return hip_fail(e, "hipMemsetAsync warm-start state");
     c->warm_batch = batch;
     c->warm_calls = 0;
@@ -287,7 +288,7 @@ static int warm_state(f110qp_ctx* c, int batch, hipStream_t s, f110qp::WarmState
   ws->key = (unsigned*)c->wkey.p;
   ws->act = (unsigned long long*)c->wact.p;
   ws->hit_call = (unsigned*)((char*)c->wkey.p + B * 16);
-  ws->stats = ws->hit_call + 1;  // [1] traffic calls, [2] hits (cumulative since the layout)
+  ws->stats = (unsigned*)((char*)c->wkey.p + B * 16 + 16);  // per wave: hits, traffic calls
   ws->call = ++c->warm_calls;
   c->warm_stream = s;
   return F110QP_OK;
@@ -376,13 +377,19 @@ int f110qp_warm_hits(f110qp_ctx* c, int* traffic, int* hits) {
   if (!c->cfg.warm_start || c->warm_batch == 0 || !c->wkey.p) return F110QP_OK;
   hipError_t e = hipStreamSynchronize(c->warm_stream);
   if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-  unsigned st[3];
-  if ((e = hipMemcpy(st, (char*)c->wkey.p + (size_t)c->warm_batch * 16, sizeof(st), hipMemcpyDeviceToHost)))
+  // per-wave counters (hits, traffic calls) of every wave of the lane launches: every wave of a call
+  // counts the same traffic, wave 0 is the call's count; the hits sum over the waves
+  const size_t nw = (size_t)c->warm_batch + 1;
+  std::vector<unsigned> st(2 * nw);
+  if ((e = hipMemcpy(st.data(), (char*)c->wkey.p + (size_t)c->warm_batch * 16 + 16, st.size() * sizeof(unsigned),
+                     hipMemcpyDeviceToHost)))
     return hip_fail(e, "hipMemcpy warm-start counters");
+  unsigned hsum = 0;
+  for (size_t w = 0; w < nw; w++) hsum += st[2 * w];
   *traffic = (int)(st[1] - c->warm_prev[0]);
-  *hits = (int)(st[2] - c->warm_prev[1]);
+  *hits = (int)(hsum - c->warm_prev[1]);
   c->warm_prev[0] = st[1];
-  c->warm_prev[1] = st[2];
+  c->warm_prev[1] = hsum;
   return F110QP_OK;
 }
 

@@ -49,8 +49,9 @@ struct WarmState {
   // which a wave saw a key hit (see warm_traffic)
   unsigned* hit_call = nullptr;
   unsigned call = 0;  // wraps after 2^32 calls: compared by unsigned difference only
-  // lane back ends: cumulative counters (f110qp_warm_hits) [0] calls that moved warm traffic,
-  // [1] QPs whose key hit; one atomic per wave, and only in a call that moves the traffic
+  // lane back ends: cumulative counters per wave w (f110qp_warm_hits), stats[2w] QPs whose key hit,
+  // stats[2w + 1] calls that moved warm traffic; read and written by the wave itself, only in a
+  // call that moves the traffic
   unsigned* stats = nullptr;
 };
 

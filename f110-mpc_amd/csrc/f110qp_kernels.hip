@@ -77,12 +77,11 @@ __global__ __launch_bounds__(256) void gap_screen_kernel(const int B, const int 
 // the launch (an atomic append in the lane kernel's wave completion order put them late; same-box
 // A/B on C3: step 236-242 -> 225 us with this order).
 constexpr int kPrioMax = 127;
-static_assert(kPrioMax + 1 == 128, "gap_order_kernel scans the priorities as two 64-lane rows");
 __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int* __restrict__ prio,
                                                          int* __restrict__ count, int* __restrict__ list,
                                                          int* __restrict__ zero) {
   __shared__ int hist[kPrioMax + 1];
-  __shared__ int off[kPrioMax + 1];
+  __shared__ int off[2][kPrioMax + 1];
   const int t = threadIdx.x;
   if (t <= kPrioMax) hist[t] = 0;
   __syncthreads();
@@ -91,33 +90,35 @@ __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int*
     if (p > 0) atomicAdd(&hist[p], 1);
   }
   __syncthreads();
-  // descending exclusive offsets (the highest priority first) by two 64-lane scans: thread
-  // t < 128 holds priority 127 - t (priority 0, not listed, contributes nothing)
-  __shared__ int wtot;
-  int inc = 0, own = 0;
-  if (t < kPrioMax + 1) {
-    own = (t < kPrioMax) ? hist[kPrioMax - t] : 0;
-    inc = own;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int o = __shfl_up(inc, d, 64);
-      inc += ((t & 63) >= d) ? o : 0;
-    }
-    if (t == 63) wtot = inc;
-  }
+  // descending offsets (the highest priority first): an inclusive scan over r = kPrioMax - p in
+  // LDS, log2(128) barrier-separated steps, independent of the wavefront width (round-5 ADVICE: the
+  // two 64-lane shuffle scans assumed wave64)
+  const int r = kPrioMax - t;  // thread t < 128 scans priority kPrioMax - t (priority 0 counts none)
+  if (t <= kPrioMax) off[0][t] = (r > 0) ? hist[r] : 0;
   __syncthreads();
-  if (t < kPrioMax + 1) {
-    if (t >= 64) inc += wtot;
-    if (t < kPrioMax) off[kPrioMax - t] = inc - own;
+  int src = 0;
+#pragma unroll
+  for (int d = 1; d <= kPrioMax; d <<= 1) {
+    if (t <= kPrioMax) off[src ^ 1][t] = off[src][t] + (t >= d ? off[src][t - d] : 0);
+    src ^= 1;
+    __syncthreads();
+  }
+  if (t <= kPrioMax) {
+    const int inc = off[src][t];
+    hist[t] = inc;  // (hist is free again) inclusive prefix in scan order
     if (t == kPrioMax) {
       *count = inc;
       if (zero) *zero = 0;  // the re-check count the GI kernel appends to next
     }
   }
   __syncthreads();
+  // exclusive offset of priority p at off[0][kPrioMax + 1 - p]: the QPs of every priority above p,
+  // i.e. the inclusive prefix at scan index kPrioMax - p - 1 (0 for the top priority)
+  if (t >= 1 && t <= kPrioMax) off[0][t] = (t >= 2) ? hist[t - 2] : 0;
+  __syncthreads();
   for (int b = t; b < B; b += 1024) {
     const int p = min(prio[b], kPrioMax);
-    if (p > 0) list[atomicAdd(&off[p], 1)] = b;
+    if (p > 0) list[atomicAdd(&off[0][kPrioMax + 1 - p], 1)] = b;
   }
 }
 

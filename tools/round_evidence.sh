@@ -7,7 +7,7 @@
 #   python tools/summarize_profiles.py r04 c2 c3 c4 c5 c2_big c4_8192 c4_16384
 #   python tools/summarize_sq.py r04 c2:lane_seg_kernel c4_8192:lane_seg_kernel c4_16384:lane_seg_kernel c3:solve_kernel
 set -o pipefail
-rnd=${1:-r05}
+rnd=${1:-r06}
 part=${2:-all}
 out=gpurun_out/$rnd
 mkdir -p $out
@@ -42,6 +42,8 @@ bash tools/sq_pass.sh c2 --config c2 || exit 9
 bash tools/sq_pass.sh c4_8192 --config c4 --batch 8192 || exit 9
 bash tools/sq_pass.sh c4_16384 --config c4 --batch 16384 || exit 9
 bash tools/sq_pass.sh c3 --config c3 || exit 9
+timeout -k 10 300 python tools/c2_growth_probe.py > $out/c2_growth_probe.txt 2>&1 || exit 10
+timeout -k 10 300 python tools/recheck_counts.py > $out/recheck_counts.json 2> $out/recheck_counts.err || exit 11
 for c in c2 c4; do  # bench.py starts its two ranks itself (gloo: both on GPU 0)
   timeout -k 10 300 python bench.py --gpus 2 --config $c --dist-backend gloo --no-cpu --no-latency --steps 20 \
     2> $out/bench_2rank_$c.err | grep "^{\"metric\"" > $out/bench_2rank_gloo_$c.json || exit 8
