@@ -267,6 +267,22 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
         stream.synchronize()
         if i >= 20:
             prep_async_t.append(time.perf_counter() - t0)
+    # the same one-QP call over 64 distinct QPs of the batch (each its own tick, 5 calls each): the
+    # latency depends on the QP's PDAS pass count (DESIGN.md 2b'), QP 0 above is one sample of it
+    nmix = min(64, int(w["x0"].shape[0]))
+    mix = {k: torch.from_numpy(np.ascontiguousarray(w[k][:nmix])).to(dev) for k in ("x0", "u_lin", "x_ref")}
+    hmix = None if hs is None else hs[:nmix].contiguous()
+    mix_l = [s1.prepare_dev(mix["x0"][i:i + 1], mix["u_lin"][i:i + 1], mix["x_ref"][i:i + 1],
+                            None if hmix is None else hmix[i:i + 1], uo, xo, st, stream=stream, sync=True)
+             for i in range(nmix)]
+    for f in mix_l:
+        f()
+    mix_t = []
+    for rep_ in range(5):
+        for f in mix_l:
+            t0 = time.perf_counter()
+            f()
+            mix_t.append(time.perf_counter() - t0)
     # the B = 1 kernel alone (HIP events over back-to-back launches)
     ea = torch.cuda.Event(enable_timing=True)
     eb = torch.cuda.Event(enable_timing=True)
@@ -292,13 +308,15 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
         stream.synchronize()
         if i >= 5:
             batch_t.append(time.perf_counter() - t0)
-    return {"single_qp_device": pct(prep_t), "single_qp_device_async_then_sync": pct(prep_async_t),
+    return {"single_qp_device": pct(prep_t), f"single_qp_device_{nmix}_qps": pct(mix_t),
+            "single_qp_device_async_then_sync": pct(prep_async_t),
             "single_qp_device_ctypes": pct(dev_t),
             "single_qp_host_pointers": pct(host_t), "batch_launch": pct(batch_t),
             "single_qp_kernel_us": k1_us,
             "single_qp_backend": ("lane" + (f" (S = {seg1})" if seg1 > 1 else "")) if be1 == capi.BACKEND_LANE else "wave",
             "note": "wall clock per call incl. launch + wait for the results: single_qp_device is one C call "
-                    "(f110qp_solve_batch_dev_sync: launch + hipStreamSynchronize), _async_then_sync the "
+                    "(f110qp_solve_batch_dev_sync: launch + hipStreamSynchronize) on QP 0 of the batch, "
+                    f"_{nmix}_qps the same call over {nmix} distinct QPs of the batch, _async_then_sync the "
                     "asynchronous launcher then torch's stream synchronize, _ctypes with the per-call argument "
                     "conversion; host-pointer path adds H2D/D2H over PCIe"}
 

@@ -1687,6 +1687,13 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           return -r2n;
         };
         float prev = 3.0e38f;
+        // the last residual evaluation when the refinement stopped on its own test: with no negative
+        // multiplier it is the certificate's clamped residual at the same point (reused below)
+        double r1k[R];
+        float w1k[R];
+        bool refok = false;
+#pragma unroll
+        for (int r = 0; r < R; r++) { r1k[r] = 0.0; w1k[r] = 0.f; }
         for (int rs = 0; rs < kRefineMax; rs++) {
           wsync();
           double r1[R];
@@ -1707,7 +1714,12 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
           rsq = wave_sum(rsq);
           float r2[R];
           const float r2n = act_res(r2);
-          if (rsq <= 0.25 * thr2 && r2n <= 1e-9f) break;  // small enough: the certificate decides below
+          if (rsq <= 0.25 * thr2 && r2n <= 1e-9f) {  // small enough: the certificate decides below
+#pragma unroll
+            for (int r = 0; r < R; r++) { r1k[r] = r1[r]; w1k[r] = w1[r]; }
+            refok = true;
+            break;
+          }
           if (rs + 1 == kRefineMax) break;
           // v1_j = n_j' w1 (= V_j' r1 with the gap rows' stored V_j = W n_j: r1 is still in sm.vec
           // from the W product, so no rollout of w1 and no barrier)
@@ -1833,18 +1845,25 @@ __device__ __forceinline__ void solve_qp(Smem<NUM, GAP>& sm, const int b, const 
             // duality gap charges them as 2 mu+ s, which measured 1e4-1e6 times the threshold on
             // exact points and is not used.
             double r1c[R];
-            wsync();
-            kkt_res(true, r1c);
+            float wc[R];
+            float r2nc = 0.f;  // (the refinement's own test held the active rows to 1e-9)
+            if (refok && __ballot(neg) == 0ull) {
 #pragma unroll
-            for (int r = 0; r < R; r++) {
-              sm.d64[vv[r]] = u64[r];
-              if (GAP && a == 1 && kk[r] < N) { sm.sx64[kk[r] + 1] = px[r]; sm.sy64[kk[r] + 1] = py[r]; }
-              sm.vec[vv[r]] = (float)r1c[r];
+              for (int r = 0; r < R; r++) { r1c[r] = r1k[r]; wc[r] = w1k[r]; }
+            } else {
+              wsync();
+              kkt_res(true, r1c);
+#pragma unroll
+              for (int r = 0; r < R; r++) {
+                sm.d64[vv[r]] = u64[r];
+                if (GAP && a == 1 && kk[r] < N) { sm.sx64[kk[r] + 1] = px[r]; sm.sy64[kk[r] + 1] = py[r]; }
+                sm.vec[vv[r]] = (float)r1c[r];
+              }
+              wsync();
+              float r2c[R];
+              matvec_W<NUM, GAP, R>(sm, lane, wc);
+              r2nc = act_res(r2c);
             }
-            wsync();
-            float wc[R], r2c[R];
-            matvec_W<NUM, GAP, R>(sm, lane, wc);
-            const float r2nc = act_res(r2c);
             const double lam = fmin(P.r[0], P.r[1]);
             double ycr[R];
 #pragma unroll
