@@ -251,8 +251,9 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
         if i >= 20:
             dev_t.append(time.perf_counter() - t0)
     # the same through the prepared launcher: one C call per tick that returns with the answer
-    # (f110qp_solve_batch_dev_sync: launch, then hipStreamSynchronize; what a C++ caller of the
-    # ABI pays), no ctypes argument conversion
+    # (f110qp_solve_batch_dev_sync: launch, then wait on the kernel's completion word, or the
+    # stream where the call is several kernels; what a C++ caller of the ABI pays), no ctypes
+    # argument conversion
     launch1s = s1.prepare_dev(one["x0"], one["u_lin"], one["x_ref"], h1, uo, xo, st, stream=stream, sync=True)
     for i in range(reps + 20):
         t0 = time.perf_counter()
@@ -301,6 +302,7 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
         s1.solve(hx["x0"], hx["u_lin"], hx["x_ref"], hh)
         if i >= 20:
             host_t.append(time.perf_counter() - t0)
+    polled = s1.sync_signals()
     s1.close()
     for i in range(min(reps, 100) + 5):
         t0 = time.perf_counter()
@@ -313,12 +315,15 @@ def measure_latency(capi, solver, cfg, w, hs, N, dev, stream, step, reps=300):
             "single_qp_device_ctypes": pct(dev_t),
             "single_qp_host_pointers": pct(host_t), "batch_launch": pct(batch_t),
             "single_qp_kernel_us": k1_us,
+            "single_qp_polled_calls": polled,
             "single_qp_backend": ("lane" + (f" (S = {seg1})" if seg1 > 1 else "")) if be1 == capi.BACKEND_LANE else "wave",
             "note": "wall clock per call incl. launch + wait for the results: single_qp_device is one C call "
-                    "(f110qp_solve_batch_dev_sync: launch + hipStreamSynchronize) on QP 0 of the batch, "
+                    "(f110qp_solve_batch_dev_sync: launch + poll of the kernel's completion word in pinned host "
+                    "memory, hipStreamSynchronize for multi-kernel gap-row calls) on QP 0 of the batch, "
                     f"_{nmix}_qps the same call over {nmix} distinct QPs of the batch, _async_then_sync the "
                     "asynchronous launcher then torch's stream synchronize, _ctypes with the per-call argument "
-                    "conversion; host-pointer path adds H2D/D2H over PCIe"}
+                    "conversion; host-pointer path: the kernel reads and writes pinned host memory (zero-copy) and "
+                    "the call polls the same completion word"}
 
 
 def _halfspaces_host(w, B):

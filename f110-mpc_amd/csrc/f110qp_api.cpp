@@ -111,6 +111,10 @@ struct f110qp_ctx {
   int lane_twin = 1;         // segmented kernel: twin PDAS starts where they fit (LaneWork::twin)
   int gap_screen = -1;      // gap rows, AUTO: box screen on the lane kernel (-1 by batch, 0 off, 1 on)
   int recheck_all = 0;      // gap rows: every QP of a call through the fp64 re-check alone (test build)
+  HostBuf hsig;              // synchronous calls: the completion word they poll (wait_done)
+  DevBuf dsig;               // its kernel's wave arrival count (zeroed once, re-zeroed by the kernel)
+  unsigned sig_seq = 0;      // number of the last signalled call (the value the kernel publishes)
+  int sig_poll = 1;          // 0: synchronous calls synchronise the stream (test build, F110QP_SIG_POLL=0)
   hipStream_t stream = nullptr;
   hipStream_t last_gap_stream = nullptr;  // stream of the last gap-row call (f110qp_last_recheck_count)
   int last_gap_batch = 0;                 // its batch (0: no gap-row call yet)
@@ -160,8 +164,58 @@ static void test_hooks(f110qp_ctx* c) {
   // gap rows: every QP of a call through the fp64 re-check (gi64_kernel.h) alone, no screen and no
   // fp32 GI: the re-check's own answers, for its parity tests
   if (env_int("F110QP_RECHECK_ALL", 0, 1, &v)) c->recheck_all = v;
+  // 0: synchronous calls wait with hipStreamSynchronize, not on the kernel's completion word
+  if (env_int("F110QP_SIG_POLL", 0, 1, &v)) c->sig_poll = v;
 }
 #endif
+
+// Synchronous calls whose work is one kernel that raises the completion signal (f110qp::launch_signals:
+// the box-only solve on the segmented lane kernel, the per-tick call) wait for that kernel's last
+// wave to write the call's number to a pinned host word instead of synchronising the stream: the
+// hipStreamSynchronize round trip measured 12.2 us p50 against 6.5 us for the polled word on an
+// empty kernel (tools/microbench/flag_latency.hip). Arms the signal in *oo when the
+// call's kernels raise it; *armed false: the caller synchronises the stream.
+static int arm_signal(f110qp_ctx* c, int batch, int backend, const float* h, const f110qp::LaneWork& lw,
+                      hipStream_t s, f110qp::ObjOut* oo, bool* armed) {
+  *armed = false;
+  if (!c->sig_poll || !f110qp::launch_signals(c->kp, batch, backend, h, lw)) return F110QP_OK;
+  if (!c->hsig.p) {
+    hipError_t e = c->hsig.ensure(64);
+    if (e != hipSuccess) return hip_fail(e, "hipHostMalloc completion word");
+    if ((e = c->dsig.ensure(64)) != hipSuccess) return hip_fail(e, "hipMalloc arrival count");
+    if ((e = hipMemsetAsync(c->dsig.p, 0, 64, s)) != hipSuccess) return hip_fail(e, "hipMemsetAsync arrival count");
+    __atomic_store_n((unsigned*)c->hsig.p, c->sig_seq, __ATOMIC_RELEASE);
+  }
+  oo->sig_host = (unsigned*)c->hsig.d;
+  oo->sig_count = (unsigned*)c->dsig.p;
+  oo->sig_seq = ++c->sig_seq;
+  *armed = true;
+  return F110QP_OK;
+}
+
+// Waits for the call armed by arm_signal (or synchronises the stream when it was not armed). The
+// poll asks the stream every 1024 reads, so a kernel that faults (no signal) is reported by its
+// HIP error, and a drained stream without the word is reported as an error, not waited on.
+static int wait_done(f110qp_ctx* c, hipStream_t s, bool armed) {
+  if (!armed) {
+    const hipError_t e = hipStreamSynchronize(s);
+    return e == hipSuccess ? F110QP_OK : hip_fail(e, "hipStreamSynchronize");
+  }
+  const unsigned seq = c->sig_seq;
+  const unsigned* w = (const unsigned*)c->hsig.p;
+  for (unsigned k = 1;; k++) {
+    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return F110QP_OK;
+    if ((k & 1023u) == 0) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return F110QP_OK;
+        return fail(F110QP_ERR_HIP, "solve kernel finished without its completion signal");
+      }
+      if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
+    }
+    __builtin_ia32_pause();
+  }
+}
 
 extern "C" {
 
@@ -401,6 +455,12 @@ int f110qp_test_build(void) {
 #endif
 }
 
+int f110qp_sync_signals(f110qp_ctx* c, unsigned* count) {
+  if (!c || !count) return fail(F110QP_ERR_INVALID, "ctx / count is NULL");
+  *count = c->sig_seq;
+  return F110QP_OK;
+}
+
 int f110qp_warm_reset(f110qp_ctx* c) {
   if (!c) return fail(F110QP_ERR_INVALID, "ctx is NULL");
   c->warm_batch = 0;  // the next call re-zeroes the slot keys
@@ -413,37 +473,41 @@ int f110qp_solve_batch_dev(f110qp_ctx* c, int batch, const float* x0, const floa
   return f110qp_solve_batch_ex_dev(c, batch, x0, ul, xr, hs, uo, xo, st, it, nullptr, nullptr, stream);
 }
 
+// device-pointer solve; sync: wait for it before returning (the completion word where the call's
+// kernel raises it, else the stream)
+static int solve_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul, const float* xr,
+                     const float* hs, float* uo, float* xo, int* st, int* it, double* obj,
+                     double* cost, hipStream_t s, bool sync) {
+  int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
+  if (rc || batch == 0) return rc;
+  const float* h = (c->cfg.gap_mode == F110QP_GAP_ACTIVE) ? hs : nullptr;
+  f110qp::WarmState ws;
+  rc = warm_state(c, batch, s, &ws);
+  if (rc) return rc;
+  int backend;
+  f110qp::LaneWork lw;
+  rc = lane_work(c, batch, s, &backend, &lw);
+  if (rc) return rc;
+  f110qp::ObjOut oo;
+  oo.obj = obj;
+  oo.cost = cost;
+  bool armed = false;
+  if (sync && (rc = arm_signal(c, batch, backend, h, lw, s, &oo, &armed))) return rc;
+  hipError_t e = f110qp::launch_solve(c->kp, batch, x0, ul, xr, h, uo, xo, st, it, ws, backend, lw, oo, s);
+  if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
+  return sync ? wait_done(c, s, armed) : F110QP_OK;
+}
+
 int f110qp_solve_batch_dev_sync(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                                 const float* xr, const float* hs, float* uo, float* xo, int* st,
                                 int* it, void* stream) {
-  const int rc = f110qp_solve_batch_ex_dev(c, batch, x0, ul, xr, hs, uo, xo, st, it, nullptr, nullptr, stream);
-  if (rc) return rc;
-  // (a hipStreamQuery spin measured slower: B = 1 p50 22.9 against 20.8 us for the synchronize)
-  const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
-  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
-  return F110QP_OK;
+  return solve_dev(c, batch, x0, ul, xr, hs, uo, xo, st, it, nullptr, nullptr, (hipStream_t)stream, true);
 }
 
 int f110qp_solve_batch_ex_dev(f110qp_ctx* c, int batch, const float* x0, const float* ul,
                               const float* xr, const float* hs, float* uo, float* xo, int* st,
                               int* it, double* obj, double* cost, void* stream) {
-  int rc = check_batch_args(c, batch, x0, ul, xr, hs, uo, xo, st);
-  if (rc || batch == 0) return rc;
-  const float* h = (c->cfg.gap_mode == F110QP_GAP_ACTIVE) ? hs : nullptr;
-  f110qp::WarmState ws;
-  rc = warm_state(c, batch, (hipStream_t)stream, &ws);
-  if (rc) return rc;
-  int backend;
-  f110qp::LaneWork lw;
-  rc = lane_work(c, batch, (hipStream_t)stream, &backend, &lw);
-  if (rc) return rc;
-  f110qp::ObjOut oo;
-  oo.obj = obj;
-  oo.cost = cost;
-  hipError_t e = f110qp::launch_solve(c->kp, batch, x0, ul, xr, h, uo, xo, st, it, ws, backend,
-                                      lw, oo, (hipStream_t)stream);
-  if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
-  return F110QP_OK;
+  return solve_dev(c, batch, x0, ul, xr, hs, uo, xo, st, it, obj, cost, (hipStream_t)stream, false);
 }
 
 // Per-group W cache of a grouped call (grows only; every call re-fills the slots it uses).
@@ -651,6 +715,7 @@ static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul
   int backend;
   f110qp::LaneWork lw;
   f110qp::ObjOut oo;
+  bool armed = false;
   oo.obj = obj ? (double*)(dq + o_ob) : nullptr;
   oo.cost = cost ? (double*)(dq + o_co) : nullptr;
   if (group) {
@@ -668,6 +733,10 @@ static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul
     f110qp::WarmState ws;
     if ((rc = warm_state(c, batch, s, &ws))) return rc;
     if ((rc = lane_work(c, batch, s, &backend, &lw))) return rc;
+    // zero-copy: the kernel's stores are the outputs the host reads, so its completion word ends
+    // the wait (staged batches wait for the D2H copy on the stream)
+    if (zc && (rc = arm_signal(c, batch, backend, gap ? (const float*)(di + o_hs) : nullptr, lw, s, &oo, &armed)))
+      return rc;
     e = f110qp::launch_solve(c->kp, batch, (const float*)di, (const float*)(di + o_ul),
                              (const float*)(di + o_xr), gap ? (const float*)(di + o_hs) : nullptr,
                              (float*)dq, (float*)(dq + o_xo), (int*)(dq + o_st), (int*)(dq + o_it),
@@ -676,8 +745,7 @@ static int solve_host(f110qp_ctx* c, int batch, const float* x0, const float* ul
   if (e != hipSuccess) return hip_fail(e, "solve kernel launch");
   if (!zc && (e = hipMemcpyAsync(c->hout.p, dq, out_bytes, hipMemcpyDeviceToHost, s)))
     return hip_fail(e, "hipMemcpyAsync D2H");
-  e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  if ((rc = wait_done(c, s, armed))) return rc;
   const char* ho = (const char*)c->hout.p;
   std::memcpy(uo, ho, s_uo);
   std::memcpy(xo, ho + o_xo, s_xo);

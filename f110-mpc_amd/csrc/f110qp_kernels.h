@@ -119,7 +119,17 @@ struct ObjOut {
   // (count + list; null: the re-check flags them itself)
   int* rc_count = nullptr;
   int* rc_list = nullptr;
+  // completion signal of a synchronous call (segmented lane kernel only, launch_signals): every
+  // wave arrives on sig_count once its stores are visible at system scope; the last one re-zeroes
+  // the count and writes sig_seq to sig_host (pinned host word the calling thread polls). null: none
+  unsigned* sig_host = nullptr;
+  unsigned* sig_count = nullptr;
+  unsigned sig_seq = 0;
 };
+
+// whether launch_solve's kernels for this call raise ObjOut's completion signal (the box-only solve
+// on the segmented lane kernel: one kernel per call); the caller synchronises the stream otherwise
+bool launch_signals(const KParams& P, int B, int backend, const float* hs, const LaneWork& lw);
 
 // waves the lane kernel's grid aims for (one per CU of the MI355X's 256)
 constexpr int kLaneTargetWaves = 256;

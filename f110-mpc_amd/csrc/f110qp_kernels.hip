@@ -130,11 +130,17 @@ __global__ __launch_bounds__(256) void list_all_kernel(const int B, int* __restr
   if (b == 0) *count = B;
 }
 
+bool launch_signals(const KParams& P, int B, int backend, const float* hs, const LaneWork& lw) {
+  return B > 0 && !hs && backend == BACKEND_LANE && lane_segments(P, B, lw) > 1;
+}
+
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
                         const float* xr, const float* hs, float* uo, float* xo, int* st,
                         int* its, const WarmState& ws, int backend, const LaneWork& lw,
-                        const ObjOut& oo, hipStream_t s) {
+                        const ObjOut& oo_in, hipStream_t s) {
   if (B <= 0) return hipSuccess;
+  ObjOut oo = oo_in;
+  if (!launch_signals(P, B, backend, hs, lw)) oo.sig_host = nullptr;  // several kernels: no signal
   if (hs) {
     // Gap rows. With the screen: the box-only lane solve of every QP (the segmented kernel
     // evaluates the screen in its output sweep, in fp64, and writes each QP's GI priority; the

@@ -92,6 +92,7 @@ EXPORTED = (
     "f110qp_last_recheck_count",
     "f110qp_lane_starts",
     "f110qp_warm_hits",
+    "f110qp_sync_signals",
     "f110qp_test_build",
 )
 SCRATCH_NAMES = {0: "none (wave back end)", 1: "LDS fp64", 2: "LDS fp32", 3: "HBM fp64", 4: "HBM fp32"}
@@ -167,6 +168,7 @@ def load(test: bool = False):
     L.f110qp_last_recheck_count.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
     L.f110qp_lane_starts.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
     L.f110qp_warm_hits.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.f110qp_sync_signals.argtypes = [C.c_void_p, C.POINTER(C.c_uint)]
     L.f110qp_test_build.restype = C.c_int
     L.f110qp_condense_debug_dev.argtypes = [C.c_void_p, C.c_int] + [fp] * 6
     L.f110qp_warm_reset.argtypes = [C.c_void_p]
@@ -316,6 +318,13 @@ class Solver:
         t, h = C.c_int(), C.c_int()
         self._chk(self.lib.f110qp_warm_hits(self._h, C.byref(t), C.byref(h)), "f110qp_warm_hits")
         return t.value, h.value
+
+    def sync_signals(self) -> int:
+        """Synchronous calls on this solver that waited on the kernel's completion word instead of
+        synchronising the stream (f110qp_sync_signals)."""
+        n = C.c_uint()
+        self._chk(self.lib.f110qp_sync_signals(self._h, C.byref(n)), "f110qp_sync_signals")
+        return n.value
 
     @property
     def test_build(self) -> bool:
