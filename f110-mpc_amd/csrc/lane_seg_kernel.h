@@ -102,6 +102,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     const ObjOut oo) {
   constexpr int twin = TWIN ? 1 : 0;
   constexpr int L = 64 / S;  // QPs per wave
+  // the kernel arguments the staging address needs, in SGPRs before anything else: hipcc loads
+  // kernel arguments next to their first use, which put two dependent kernarg round trips in
+  // front of the staging loads
   constexpr int NV = FST ? 14 : 11;  // scratch doubles per stage: K 6, k 2, then F 6 or S^-1 3
   extern __shared__ __attribute__((aligned(16))) double seg_smem[];
   const int lane = threadIdx.x;
@@ -231,14 +234,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   SSTAMP(t_lin);
   // references of the lane's stages: recentred (ROT: rotated) fp64, lane-major; a non-finite
   // entry flags the QP (one ballot folded over its segment lanes)
+  // (the loop runs to the wave-uniform mM: a lane of a shorter segment converts one stage of the
+  // next segment, or of the staging's junk rows on the top segment, into a row it never reads, so
+  // the loop has no EXEC-masked exits; its flag only counts stages < m)
   bool nonfin = false;
   {
     const float* stg = reinterpret_cast<const float*>(lbase + o_sc);
-    for (int t = 0; t < m; t++) {
+    for (int t = 0; t < mM; t++) {
       const int i = s0 + t;
       const float fx = stg[(3 * i + 0) * L + slot], fy = stg[(3 * i + 1) * L + slot];
       const float ft = stg[(3 * i + 2) * L + slot];
-      nonfin |= !(isfinite(fx) && isfinite(fy) && isfinite(ft));
+      nonfin |= (t < m) & !(isfinite(fx) && isfinite(fy) && isfinite(ft));
       const double dx = (double)fx - X0, dy = (double)fy - Y0;
       r64[(3 * t + 0) * 64] = ROT ? cs * dx + sn * dy : dx;
       r64[(3 * t + 1) * 64] = ROT ? cs * dy - sn * dx : dy;
@@ -256,42 +262,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   const int R = (2 * N + 63) / 64;
   const unsigned kth = __float_as_uint(fTH0), kv = __float_as_uint(fv), kd = __float_as_uint(fd);
   {
-    unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
 #ifdef F110QP_SEG_SEED_ANY  // measurement knob: seed from the slot's previous set on any key
                             // (measured C5 31.2 -> 34.9 us: the stale set costs passes)
     const bool hit = wt && key3 != 0u;
 #else
     const bool hit = wt && key3 != 0u && key0 == kth && key1 == kv && key2 == kd;
 #endif
-    if (ws.hit_call && __ballot(hit) != 0ull && lane == 0) *ws.hit_call = ws.call;
-    wst.x += (unsigned)__popcll(__ballot(hit && qowner0 && !var));  // hits (one lane per QP)
-    if (hit) {
-      lo0 = ws.act[2 * R * b];
-      hi0 = ws.act[2 * R * b + 1];
-      if (R > 1) {
-        lo1 = ws.act[2 * (R * b + 1)];
-        hi1 = ws.act[2 * (R * b + 1) + 1];
+    unsigned long long lw = 0, hw = 0;
+    if (wt) {  // (wave-uniform: a call that moves no warm state skips the mask window)
+      if (ws.hit_call && __ballot(hit) != 0ull && lane == 0) *ws.hit_call = ws.call;
+      wst.x += (unsigned)__popcll(__ballot(hit && qowner0 && !var));  // hits (one lane per QP)
+      unsigned long long lo0 = 0, lo1 = 0, hi0 = 0, hi1 = 0;
+      if (hit) {
+        lo0 = ws.act[2 * R * b];
+        hi0 = ws.act[2 * R * b + 1];
+        if (R > 1) {
+          lo1 = ws.act[2 * (R * b + 1)];
+          hi1 = ws.act[2 * (R * b + 1) + 1];
+        }
       }
-    }
-    // the lane's 2m mask bits start at bit 2 s0 of the 128-bit pair (hi word : lo word)
-    const int sh = 2 * s0;
-    auto window = [&](unsigned long long w0, unsigned long long w1) {
-      return sh >= 64 ? (w1 >> (sh - 64)) : (sh == 0 ? w0 : ((w0 >> sh) | (w1 << (64 - sh))));
-    };
-    const unsigned long long lw = window(lo0, lo1), hw = window(hi0, hi1);
-    for (int t = 0; t < m; t++) {  // per input: 1 lower, 2 upper, 0 free; the lower bound wins
-      const unsigned l2 = (unsigned)(lw >> (2 * t)) & 3u, h2 = (unsigned)(hw >> (2 * t)) & 3u & ~l2;
-      ap[t * 64] = (int)((l2 & 1u) | ((h2 & 1u) << 1) | ((l2 & 2u) << 1) | ((h2 & 2u) << 2));
+      // the lane's 2m mask bits start at bit 2 s0 of the 128-bit pair (hi word : lo word)
+      const int sh = 2 * s0;
+      auto window = [&](unsigned long long w0, unsigned long long w1) {
+        return sh >= 64 ? (w1 >> (sh - 64)) : (sh == 0 ? w0 : ((w0 >> sh) | (w1 << (64 - sh))));
+      };
+      lw = window(lo0, lo1);
+      hw = window(hi0, hi1);
     }
     // the twin start: the speed bound u_des sits on, active on the first half of the horizon (on
     // the C2 / C5 workloads the optimum holds the speed on its upper bound over a prefix of the
     // horizon that cold PDAS finds a few stages per pass: numpy model of the kernel's PDAS, the
     // slowest QP's passes 4-5 -> 3-4 over eight C2 batches and six C5 ticks; launch_lane_seg_t
     // enables it only when u_des is on a speed bound)
-    if (var && !hit) {
-      const int sv = ud0 >= ub0 ? 2 : (ud0 <= lb0 ? 1 : 0);
-      for (int t = 0; t < m; t++)
-        if (2 * (s0 + t) < N) ap[t * 64] = sv;
+    const int sv = ud0 >= ub0 ? 2 : (ud0 <= lb0 ? 1 : 0);
+    const bool tw = var && !hit;
+    // per input: 1 lower, 2 upper, 0 free; the lower bound wins. To the wave-uniform mM (rows
+    // t >= m of a shorter segment are never read): no EXEC-masked loop exits
+    for (int t = 0; t < mM; t++) {
+      const unsigned l2 = (unsigned)(lw >> (2 * t)) & 3u, h2 = (unsigned)(hw >> (2 * t)) & 3u & ~l2;
+      const int a = (int)((l2 & 1u) | ((h2 & 1u) << 1) | ((l2 & 2u) << 1) | ((h2 & 2u) << 2));
+      ap[t * 64] = (tw && 2 * (s0 + t) < N) ? sv : a;
     }
   }
 

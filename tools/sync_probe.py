@@ -45,7 +45,7 @@ def main():
 
     for poll in ((1, 0) if a.poll < 0 else (a.poll,)):
         os.environ["F110QP_SIG_POLL"] = str(poll)
-        s = capi.Solver(capi.default_config(N), test_build=True)
+        s = capi.Solver(capi.default_config(N), test_build=(poll == 0))  # the knob needs the test build
         f = s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], None, uo, xo, st, stream=stream, sync=True)
         g = s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], None, uo, xo, st, stream=stream)
         for _ in range(50):
