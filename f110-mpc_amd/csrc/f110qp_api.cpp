@@ -294,6 +294,10 @@ int f110qp_create(f110qp_ctx** out, const f110qp_config* cfg) {
 
 void f110qp_destroy(f110qp_ctx* c) {
   if (!c) return;
+  // a synchronous call returns on its completion word while its kernel may still be retiring: let
+  // it finish before the word and the arrival count are freed (the caller's stream may be gone)
+  if (c->sig_seq) (void)hipDeviceSynchronize();
+  c->hsig.release(); c->dsig.release();
   c->hin.release(); c->hout.release(); c->din.release(); c->dout.release();
   c->wW.release(); c->wkey.release(); c->wact.release();
   c->lscr.release();

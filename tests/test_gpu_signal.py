@@ -163,3 +163,26 @@ def test_multi_kernel_calls_are_not_armed(capi, knob):
         assert s.sync_signals() == 0
     seq.close()
     gap.close()
+
+
+def test_destroy_right_after_a_polled_call(capi):
+    """f110qp_destroy right after a call that returned on its completion word (the kernel may still
+    be retiring): the context waits for the device before it frees the word and the count; 30
+    create / solve / destroy cycles with the answers checked against a long-lived solver."""
+    import torch
+    N, B = 20, 8
+    w = workload.make_batch(B, N, seed=77)
+    d = _dev_inputs(torch, w)
+    ref = capi.Solver(capi.default_config(N))
+    want = ref.solve(w["x0"], w["u_lin"], w["x_ref"])
+    for k in range(30):
+        s = capi.Solver(capi.default_config(N))
+        o = _dev_outputs(torch, B, N)
+        torch.cuda.current_stream().synchronize()
+        s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], None, *o, sync=True)()
+        assert s.sync_signals() == 1
+        s.close()
+        got = [t.cpu().numpy() for t in o]
+        for p, q in zip(got, want):
+            np.testing.assert_array_equal(p, q)
+    ref.close()
