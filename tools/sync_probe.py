@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--pool", type=int, default=64, help="make_batch size the QP is taken from")
     ap.add_argument("--poll", type=int, default=-1, help="1 / 0: only the completion word / only the stream")
+    ap.add_argument("--host", action="store_true",
+                    help="host-pointer calls instead (zero-copy staging), completion word against stream sync")
     a = ap.parse_args()
     import torch
 
@@ -43,6 +45,21 @@ def main():
         return {"p50_us": round(float(np.percentile(v, 50)), 2), "p99_us": round(float(np.percentile(v, 99)), 2),
                 "min_us": round(float(v[0]), 2)}
 
+    if a.host:
+        hx = {k: np.ascontiguousarray(w[k][:B]) for k in ("x0", "u_lin", "x_ref")}
+        for poll in (1, 0):
+            os.environ["F110QP_SIG_POLL"] = str(poll)
+            s = capi.Solver(capi.default_config(N), test_build=True)
+            for _ in range(50):
+                s.solve(hx["x0"], hx["u_lin"], hx["x_ref"])
+            back = []
+            for i in range(a.reps):
+                t0 = time.perf_counter()
+                s.solve(hx["x0"], hx["u_lin"], hx["x_ref"])
+                back.append(time.perf_counter() - t0)
+            print(json.dumps({"host": True, "poll": poll, "signals": s.sync_signals(), "back_to_back": pct(back)}))
+            s.close()
+        return
     for poll in ((1, 0) if a.poll < 0 else (a.poll,)):
         os.environ["F110QP_SIG_POLL"] = str(poll)
         s = capi.Solver(capi.default_config(N), test_build=(poll == 0))  # the knob needs the test build
