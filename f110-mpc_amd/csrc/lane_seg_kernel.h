@@ -35,7 +35,8 @@
 // lane_kernel.h's. Per pass the chain is m stages of ~(200 + 120 + 30) instructions plus
 // 2 (S - 1) segment steps instead of N stages of ~255.
 //
-// Layout (fp64 throughout): lane l = slot + L j works on QP L w + slot, segment j. LDS per wave,
+// Layout (fp64 throughout): lane l = S slot + j works on QP L w + slot, segment j (a QP's segments
+// are adjacent lanes: its segment-end exchanges stay inside a quad at S <= 4). LDS per wave,
 // lane-major so that every access is one conflict-free 64-lane row: references [3m][64] (recentred,
 // rotated), PDAS state [m][64] int, Riccati scratch [m][11][64] (K 6, k 2, S^-1 3); the float
 // staging of the references borrows the scratch region.
@@ -73,9 +74,33 @@ struct SegMode {
   static constexpr int value = M;
 };
 
+// Lane-adjacent segments (lane = S slot + segment): the segment ring of a QP is S consecutive lanes,
+// so at S <= 4 the segment-end exchanges are quad permutes (DPP, a VALU move) instead of
+// ds_bpermute round trips through the LDS crossbar; S = 8 keeps ds_bpermute inside its 8-lane group.
+// Either way a lane only ever reads lanes of its own QP.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)dpp_i<CTRL>((int)(unsigned)b);
+  const unsigned hi = (unsigned)dpp_i<CTRL>((int)(unsigned)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// the value of segment + 1 (seg_up) / segment - 1 (seg_dn) of the lane's QP, round the QP's ring
 template <int S>
-__device__ __forceinline__ double seg_shfl(double v, int src) {
-  return __shfl(v, src, 64);
+__device__ __forceinline__ double seg_up(double v, int lane) {
+  if constexpr (S == 2) return dpp_d<0xB1>(v);       // quad_perm [1, 0, 3, 2]
+  else if constexpr (S == 4) return dpp_d<0x39>(v);  // quad_perm [1, 2, 3, 0]
+  else return __shfl(v, (lane & ~(S - 1)) | ((lane + 1) & (S - 1)), 64);
+}
+template <int S>
+__device__ __forceinline__ double seg_dn(double v, int lane) {
+  if constexpr (S == 2) return dpp_d<0xB1>(v);
+  else if constexpr (S == 4) return dpp_d<0x93>(v);  // quad_perm [3, 0, 1, 2]
+  else return __shfl(v, (lane & ~(S - 1)) | ((lane - 1) & (S - 1)), 64);
 }
 
 #ifndef F110QP_SEG_NEWTON
@@ -108,8 +133,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   constexpr int NV = FST ? 14 : 11;  // scratch doubles per stage: K 6, k 2, then F 6 or S^-1 3
   extern __shared__ __attribute__((aligned(16))) double seg_smem[];
   const int lane = threadIdx.x;
-  const int sl = lane & (L - 1);
-  const int seg = lane / L;
+  const int sl = lane / S;         // QP slot of the wave
+  const int seg = lane & (S - 1);  // segment: the QP's S segments are S consecutive lanes
   // twin = 1: every QP is solved from two PDAS starts at once, adjacent slots 2b (cold) and 2b + 1
   // (the speed bound nearest u_des active on the first half of the horizon); the QP is done when
   // either start has converged, and the converged one (the cold one on a tie) writes the outputs.
@@ -132,7 +157,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   const int s0 = seg * q + (seg < rem ? seg : rem);
   const int mM = q + (rem > 0 ? 1 : 0);
   const bool top = seg == S - 1;
-  const int up = (lane + L) & 63, dn = (lane - L) & 63;  // same QP, segment + 1 / - 1 (ring)
 
   SSTAMP(t_start);
 #ifdef F110QP_STAMPS
@@ -254,9 +278,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   }
   SSTAMP(t_conv);
   // terminal reference x_ref[N-1] (mpc.cpp:228): the last stage of the top segment
-  const double rNx = __shfl(r64[(3 * (m - 1) + 0) * 64], (lane | (63 & ~(L - 1))) & 63);
-  const double rNy = __shfl(r64[(3 * (m - 1) + 1) * 64], (lane | (63 & ~(L - 1))) & 63);
-  const double rNt = __shfl(r64[(3 * (m - 1) + 2) * 64], (lane | (63 & ~(L - 1))) & 63);
+  const double rNx = __shfl(r64[(3 * (m - 1) + 0) * 64], lane | (S - 1));
+  const double rNy = __shfl(r64[(3 * (m - 1) + 1) * 64], lane | (S - 1));
+  const double rNt = __shfl(r64[(3 * (m - 1) + 2) * 64], lane | (S - 1));
 
   // warm start: previous tick's active bounds when the slot's (theta0, v, steer) bits repeat
   const int R = (2 * N + 63) / 64;
@@ -305,14 +329,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     }
   }
 
-  // wave-uniform fold of a ballot over the QP's S lanes: bit sl set if any segment's bit is
-  auto fold = [&](unsigned long long mk) {
-#pragma unroll
-    for (int k = L; k < 64; k <<= 1) mk |= mk >> k;
-    return mk;
-  };
+  // whether any of the lane's QP's S lanes has its bit set in a ballot
+  auto qany = [&](unsigned long long mk) { return ((mk >> (sl * S)) & ((1ull << S) - 1ull)) != 0ull; };
   const bool bad = !(isfinite(X0) && isfinite(Y0) && isfinite(th0) && isfinite(v) && isfinite(d)) ||
-                   ((fold(__ballot(nonfin)) >> sl) & 1ull);
+                   qany(__ballot(nonfin));
   bool done = bad;
   int iters = 0;
   // the segment's start state and terminal multiplier lam_j of the current pass (kept for the
@@ -325,11 +345,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   t_setup = __builtin_amdgcn_s_memtime() - t_start;
 #endif
   for (int pass = 0; pass < max_pass; pass++) {
-    // a QP is finished when one of its starts is (twin: the sibling start is the next lane). The
+    // a QP is finished when one of its starts is (twin: the sibling start is S lanes over). The
     // shuffle runs on every lane: under a short-circuit || the done lanes are off in EXEC, and a
     // permute reads nothing from an inactive source lane
     if constexpr (TWIN) {
-      const int sib = __shfl_xor((int)done, 1, 64);
+      const int sib = __shfl_xor((int)done, S, 64);
       if (__ballot(!(done || sib != 0)) == 0ull) break;
     } else {
       if (__ballot(!done) == 0ull) break;
@@ -470,9 +490,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       double t0 = 0, t1 = 0, t2 = 0;
 #pragma unroll 1
       for (int it = 0; it < S - 1; it++) {
-        const double N00 = seg_shfl<S>(M00, up), N01 = seg_shfl<S>(M01, up), N02 = seg_shfl<S>(M02, up);
-        const double N11 = seg_shfl<S>(M11, up), N12 = seg_shfl<S>(M12, up), N22 = seg_shfl<S>(M22, up);
-        const double n0 = seg_shfl<S>(m0, up), n1 = seg_shfl<S>(m1, up), n2 = seg_shfl<S>(m2, up);
+        const double N00 = seg_up<S>(M00, lane), N01 = seg_up<S>(M01, lane), N02 = seg_up<S>(M02, lane);
+        const double N11 = seg_up<S>(M11, lane), N12 = seg_up<S>(M12, lane), N22 = seg_up<S>(M22, lane);
+        const double n0 = seg_up<S>(m0, lane), n1 = seg_up<S>(m1, lane), n2 = seg_up<S>(m2, lane);
         // Z = I - Mn Gam
         const double Z00 = 1.0 - (N00 * G00 + N01 * G01 + N02 * G02);
         const double Z01 = -(N00 * G01 + N01 * G11 + N02 * G12);
@@ -529,9 +549,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         const double e0 = F00 * xs0 + F01 * xs1 + F02 * xs2 + s0v + G00 * l0 + G01 * l1 + G02 * l2;
         const double e1 = F10 * xs0 + F11 * xs1 + F12 * xs2 + s1v + G01 * l0 + G11 * l1 + G12 * l2;
         const double e2 = F20 * xs0 + F21 * xs1 + F22 * xs2 + s2v + G02 * l0 + G12 * l1 + G22 * l2;
-        xs0 = seg_shfl<S>(e0, dn);
-        xs1 = seg_shfl<S>(e1, dn);
-        xs2 = seg_shfl<S>(e2, dn);
+        xs0 = seg_dn<S>(e0, lane);
+        xs1 = seg_dn<S>(e1, lane);
+        xs2 = seg_dn<S>(e2, lane);
       }
       lm0 = top ? 0.0 : T00 * xs0 + T01 * xs1 + T02 * xs2 + t0;
       lm1 = top ? 0.0 : T10 * xs0 + T11 * xs1 + T12 * xs2 + t1;
@@ -661,7 +681,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     if (single) {
       int mn = fi;
 #pragma unroll
-      for (int k = L; k < 64; k <<= 1) {
+      for (int k = 1; k < S; k <<= 1) {
         const int o = __shfl_xor(mn, k, 64);
         mn = o < mn ? o : mn;
       }
@@ -670,7 +690,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         changed = false;
       }
     }
-    const bool qchanged = (fold(__ballot(changed)) >> sl) & 1ull;
+    const bool qchanged = qany(__ballot(changed));
     SACC(acc_fw, t_fw);
     if (!qchanged && !done) {
       done = true;
@@ -683,8 +703,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   // iteration count while its wave sweeps on), the cold one on a tie or when neither converged
   bool owner = owner0, qowner = qowner0;
   if constexpr (TWIN) {
-    const bool sdone = __shfl_xor((int)done, 1, 64) != 0;
-    const int sibit = __shfl_xor(iters, 1, 64);
+    const bool sdone = __shfl_xor((int)done, S, 64) != 0;
+    const int sibit = __shfl_xor(iters, S, 64);
     const bool win = var ? (done && (!sdone || iters < sibit)) : (done ? (!sdone || iters <= sibit) : !sdone);
     owner = owner0 && win;
     qowner = qowner0 && win;
@@ -760,7 +780,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   }
   if (want_obj) {
 #pragma unroll
-    for (int k = L; k < 64; k <<= 1) {
+    for (int k = 1; k < S; k <<= 1) {
       J += __shfl_xor(J, k, 64);
       Cr += __shfl_xor(Cr, k, 64);
     }
@@ -773,7 +793,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     // the QP's violation count over its S lanes; GI priority 1 + count (the list is ordered by it,
     // heavy first: gap_order_kernel), 1 for a violated stage-0 row or a box solve that failed
 #pragma unroll
-    for (int k = L; k < 64; k <<= 1) nviol += __shfl_xor(nviol, k, 64);
+    for (int k = 1; k < S; k <<= 1) nviol += __shfl_xor(nviol, k, 64);
     const bool ok0 = (ga0 * X0 + gb0 * Y0 >= -gc0 - 1e-9) & (ga1 * X0 + gb1 * Y0 >= -gc1 - 1e-9);
     if (qowner) oo.scr_prio[b] = (!solved || !ok0) ? 1 : (nviol > 0 ? 1 + nviol : 0);
   }
@@ -795,7 +815,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     unsigned long long lo1 = sh == 0 ? 0ull : (sh < 64 ? lw >> (64 - sh) : lw << (sh - 64));
     unsigned long long hi1 = sh == 0 ? 0ull : (sh < 64 ? hw >> (64 - sh) : hw << (sh - 64));
 #pragma unroll
-    for (int k = L; k < 64; k <<= 1) {
+    for (int k = 1; k < S; k <<= 1) {
       lo0 |= __shfl_xor(lo0, k, 64);
       hi0 |= __shfl_xor(hi0, k, 64);
       lo1 |= __shfl_xor(lo1, k, 64);
