@@ -75,12 +75,12 @@ struct SegMode {
 };
 
 // Lane-adjacent segments (lane = S slot + segment): the segment ring of a QP is S consecutive lanes,
-// so at S <= 4 the segment-end exchanges are quad permutes (DPP, a VALU move) instead of
-// ds_bpermute round trips through the LDS crossbar; S = 8 keeps ds_bpermute inside its 8-lane group.
-// Either way a lane only ever reads lanes of its own QP.
+// so the segment-end exchanges are DPP moves (VALU) instead of ds_bpermute round trips through the
+// LDS crossbar: quad permutes at S <= 4, at S = 8 two row shifts and a select (an 8-lane group is
+// half a DPP row). A lane only ever reads lanes of its own QP.
 template <int CTRL>
 __device__ __forceinline__ int dpp_i(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);  // (an invalid source lane reads 0)
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
@@ -92,15 +92,23 @@ __device__ __forceinline__ double dpp_d(double v) {
 // the value of segment + 1 (seg_up) / segment - 1 (seg_dn) of the lane's QP, round the QP's ring
 template <int S>
 __device__ __forceinline__ double seg_up(double v, int lane) {
+  static_assert(S == 2 || S == 4 || S == 8, "segments per QP: 2, 4 or 8");
   if constexpr (S == 2) return dpp_d<0xB1>(v);       // quad_perm [1, 0, 3, 2]
   else if constexpr (S == 4) return dpp_d<0x39>(v);  // quad_perm [1, 2, 3, 0]
-  else return __shfl(v, (lane & ~(S - 1)) | ((lane + 1) & (S - 1)), 64);
+  else {  // row_shr:7 for the top lane of the group, row_shl:1 for the others; both moves run on
+          // every lane (a DPP move under a divergent branch reads inactive lanes as invalid)
+    const double a = dpp_d<0x117>(v), b = dpp_d<0x101>(v);
+    return (lane & 7) == 7 ? a : b;
+  }
 }
 template <int S>
 __device__ __forceinline__ double seg_dn(double v, int lane) {
   if constexpr (S == 2) return dpp_d<0xB1>(v);
   else if constexpr (S == 4) return dpp_d<0x93>(v);  // quad_perm [3, 0, 1, 2]
-  else return __shfl(v, (lane & ~(S - 1)) | ((lane - 1) & (S - 1)), 64);
+  else {  // row_shl:7 for segment 0 of the group, row_shr:1 for the others
+    const double a = dpp_d<0x107>(v), b = dpp_d<0x111>(v);
+    return (lane & 7) == 0 ? a : b;
+  }
 }
 
 #ifndef F110QP_SEG_NEWTON
