@@ -888,16 +888,22 @@ inline int seg_scratch_mode(const KParams& P, int B, int S, const LaneWork& lw) 
 
 // Twin starts (lane_seg_kernel<..., TWIN = true>): each QP solved from the cold start and from the
 // speed bound u_des sits on held over the first half of the horizon, in adjacent slots of one wave.
-// Taken when u_des is on a speed bound (the shipped params.yaml:42,46: des_vel = umax) and the
-// doubled grid is still at most one wave per CU: C2 (1,024 QPs, 128 waves) 26.4 -> 23.4 us, but C5
-// (4,096, 512 waves, two per CU) 28.8 -> 30.9 although its slowest tick's passes went 5 -> 4 (same
-// box). lw.twin = 0 (test build, F110QP_LANE_TWIN=0) turns it off.
-constexpr long kTwinMaxWaves = 256;
+// Taken when u_des is on a speed bound (the shipped params.yaml:42,46: des_vel = umax), the doubled
+// grid is at most two waves per CU and the lam-gain (FST) scratch of those waves fits a CU's LDS:
+// C2 (1,024 QPs, 128 waves) 26.4 -> 23.4 us. C5 (4,096, 512 waves, two per CU) measured 28.8 ->
+// 30.9 while the segment ends went through ds_bpermute, and 28.95 -> 28.55 us (cold 28.84 -> 28.3)
+// with the DPP exchanges (same box; its slowest tick's passes 5 -> 4). lw.twin = 0 (test build,
+// F110QP_LANE_TWIN=0) turns it off.
+#ifndef F110QP_TWIN_MAX_WAVES
+#define F110QP_TWIN_MAX_WAVES 512  // (measurement builds: tools/build_seg_variant.sh -D...)
+#endif
+constexpr long kTwinMaxWaves = F110QP_TWIN_MAX_WAVES;
 inline bool seg_twin(const KParams& P, int B, int S, const LaneWork& lw) {
   if (!lw.twin || !(P.udes[0] >= (double)P.umax[0] || P.udes[0] <= (double)P.umin[0])) return false;
   const long waves2 = (2L * B * S + 63) / 64;
+  const long per_cu = (waves2 + 255) / 256;
   return waves2 <= kTwinMaxWaves && seg_scratch_mode(P, 2 * B, S, lw) == 1 && lw.dref &&
-         seg_lds_bytes(P.N, S, true) <= 160 * 1024;  // the lam-gain (FST) kernel, one wave per CU
+         per_cu * seg_lds_bytes(P.N, S, true) <= 160 * 1024;  // the FST kernel, all waves resident
 }
 
 template <int S, bool ROT, bool SCR>

@@ -256,7 +256,7 @@ def test_c4_16384_per_gpu_auto(oracle, capi):
     assert rel_err(u[idx], ur).max() <= 2e-6 and rel_err(x[idx], xr).max() <= 2e-6
 
 
-@pytest.mark.parametrize("N,B", [(20, 1024), (20, 2048), (20, 4096), (30, 1000), (40, 512), (20, 1)])
+@pytest.mark.parametrize("N,B", [(20, 1024), (20, 2048), (20, 4096), (20, 8192), (30, 1000), (40, 512), (20, 1)])
 def test_twin_starts_match_one_start(oracle, capi, knob, N, B):
     """Twin starts (f110qp_lane_starts = 2: every QP also solved from the speed bound u_des sits on
     held over the first half of the horizon, the first start to converge answers): the same statuses
@@ -272,8 +272,11 @@ def test_twin_starts_match_one_start(oracle, capi, knob, N, B):
                                                                            objective=True))
         s.close()
     (n2, S2, u2, x2, s2, it2, ob2, co2), (n1, S1, u1, x1, s1, it1, ob1, co1) = out["1"], out["0"]
-    # twin where the doubled grid is at most one wave per CU (256 waves; lane_seg_kernel.h seg_twin)
-    assert n1 == 1 and S2 == S1 and (n2 == 2) == (S1 > 1 and 2 * B * S1 <= 256 * 64), (n1, n2, S1, S2)
+    # twin where the doubled grid is at most two waves per CU and their lam-gain scratch fits the CU's
+    # LDS (lane_seg_kernel.h seg_twin: 512 waves, 14 fp64 + 3 fp64 + 1 int per stage and lane)
+    waves2 = -(-2 * B * S1 // 64)
+    fits = -(-waves2 // 256) * -(-N // max(S1, 1)) * 64 * (3 * 8 + 4 + 14 * 8) <= 160 * 1024
+    assert n1 == 1 and S2 == S1 and (n2 == 2) == (S1 > 1 and waves2 <= 512 and fits), (n1, n2, S1, S2)
     np.testing.assert_array_equal(s2, s1)
     assert (s2 == capi.SOLVED).all()
     assert rel_err(u2, u1.astype(np.float64)).max() <= 1e-6 and rel_err(x2, x1.astype(np.float64)).max() <= 1e-6
