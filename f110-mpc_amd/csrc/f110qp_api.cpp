@@ -6,6 +6,7 @@
 // No C++ exception crosses this boundary.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -194,8 +195,10 @@ static int arm_signal(f110qp_ctx* c, int batch, int backend, const float* h, con
 }
 
 // Waits for the call armed by arm_signal (or synchronises the stream when it was not armed). The
-// poll asks the stream every 1024 reads, so a kernel that faults (no signal) is reported by its
-// HIP error, and a drained stream without the word is reported as an error, not waited on.
+// poll reads only the word for its first 200 us (a hipStreamQuery inside the usual 10-15 us wait
+// delayed the answer by its own cost); from then on it asks the stream every 256 reads, so a
+// kernel that faults (no word) is reported by its HIP error, and a drained stream without the word
+// is reported as an error, not waited on.
 static int wait_done(f110qp_ctx* c, hipStream_t s, bool armed) {
   if (!armed) {
     const hipError_t e = hipStreamSynchronize(s);
@@ -203,15 +206,20 @@ static int wait_done(f110qp_ctx* c, hipStream_t s, bool armed) {
   }
   const unsigned seq = c->sig_seq;
   const unsigned* w = (const unsigned*)c->hsig.p;
+  const auto t0 = std::chrono::steady_clock::now();
+  bool query = false;
   for (unsigned k = 1;; k++) {
     if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return F110QP_OK;
-    if ((k & 1023u) == 0) {
-      const hipError_t q = hipStreamQuery(s);
-      if (q == hipSuccess) {
-        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return F110QP_OK;
-        return fail(F110QP_ERR_HIP, "solve kernel finished without its completion signal");
+    if ((k & 255u) == 0) {
+      if (!query) query = std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200);
+      if (query) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) {
+          if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return F110QP_OK;
+          return fail(F110QP_ERR_HIP, "solve kernel finished without its completion signal");
+        }
+        if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
       }
-      if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
     }
     __builtin_ia32_pause();
   }
