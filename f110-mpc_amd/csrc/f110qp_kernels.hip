@@ -131,7 +131,9 @@ __global__ __launch_bounds__(256) void list_all_kernel(const int B, int* __restr
 }
 
 bool launch_signals(const KParams& P, int B, int backend, const float* hs, const LaneWork& lw) {
-  return B > 0 && !hs && backend == BACKEND_LANE && lane_segments(P, B, lw) > 1;
+  // gap rows: the call's last kernel is the fp64 re-check (launch_gap_recheck), which signals; box
+  // rows: the segmented lane kernel when it is the call's only kernel
+  return B > 0 && (hs != nullptr || (backend == BACKEND_LANE && lane_segments(P, B, lw) > 1));
 }
 
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,
@@ -150,17 +152,19 @@ hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* u
     // does not certify (SOLVED) to the re-check list, and the fp64 GI re-checks them.
     const HandLayout H(lw.hand, B);
     hipError_t e = hipSuccess;
+    ObjOut base = oo;  // the kernels before the re-check never raise the completion signal
+    base.sig_host = nullptr;
     if (lw.recheck_all) {  // test build: the re-check's own answer for every QP (no screen, no fp32 GI)
       hipLaunchKernelGGL(list_all_kernel, dim3((B + 255) / 256), dim3(256), 0, s, B, H.c_rc, H.rc);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       return launch_gap_recheck(P, B, x0, ul, xr, hs, uo, xo, st, its, H.rc, H.c_rc, oo, s);
     }
-    ObjOut go = oo;
+    ObjOut go = base;
     go.rc_count = H.c_rc;
     go.rc_list = H.rc;
     if (lw.screen) {
       const bool fused = lane_segments(P, B, lw) > 1;
-      ObjOut so = oo;
+      ObjOut so = base;
       if (fused) {
         so.scr_hs = hs;
         so.scr_prio = H.prio;
@@ -227,6 +231,7 @@ hipError_t launch_solve_grouped(const KParams& P, int B, const float* x0, const 
   if (hs) {
     const HandLayout H(lw.hand, B);
     ObjOut go = oo;
+    go.sig_host = nullptr;  // (grouped calls are never armed; only the re-check could signal)
     go.rc_count = H.c_rc;
     go.rc_list = H.rc;
     if ((e = hipMemsetAsync(H.c_rc, 0, sizeof(int), s)) != hipSuccess) return e;

@@ -132,10 +132,11 @@ def test_signal_across_streams_and_entry_points(capi):
     fresh.close()
 
 
-def test_multi_kernel_calls_are_not_armed(capi, knob):
-    """Gap rows (lane screen, order, GI, re-check: several kernels) and the sequential lane kernel
-    (F110QP_LANE_SEG=1) do not raise the signal: their synchronous calls wait on the stream, and
-    the answers equal the asynchronous entry point's."""
+def test_gap_calls_signal_from_the_recheck_and_sequential_calls_are_not_armed(capi, knob):
+    """Gap rows (lane screen or not, GI, then the fp64 re-check: several kernels) are armed, and the
+    re-check kernel, the call's last, raises the signal from its last workgroup; the sequential lane
+    kernel (F110QP_LANE_SEG=1) is not armed and synchronises the stream. Either way the answers equal
+    the asynchronous entry point's, on the device and through host pointers."""
     import torch
     B = 64
     knob("F110QP_LANE_SEG", 1)
@@ -148,7 +149,7 @@ def test_multi_kernel_calls_are_not_armed(capi, knob):
     hs[:, :, 2] = 1.0  # 0 x + 0 y >= -1: rows that never bind
     d = _dev_inputs(torch, w)
     dh = torch.from_numpy(hs).cuda()
-    for s, h in ((seq, None), (gap, dh)):
+    for s, h, armed in ((seq, None, 0), (gap, dh, 2)):
         o1, o2 = _dev_outputs(torch, B, N), _dev_outputs(torch, B, N)
         s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], h, *o1, sync=True)()
         r1 = [t.cpu().numpy() for t in o1]
@@ -160,9 +161,41 @@ def test_multi_kernel_calls_are_not_armed(capi, knob):
         assert (r1[2] == capi.SOLVED).all()
         u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs if h is not None else None)
         np.testing.assert_array_equal(u, r1[0])
-        assert s.sync_signals() == 0
+        assert s.sync_signals() == armed
     seq.close()
     gap.close()
+
+
+@pytest.mark.parametrize("screen", ["0", "1"])
+def test_gap_call_signal_with_rechecked_qps(capi, knob, screen):
+    """A synchronous gap-row call whose re-check list is not empty (the N = 48 stiff golden fixture:
+    GI leaves QPs uncertified), with and without the box screen: the completion word comes from the
+    re-check's last workgroup after every listed QP is rewritten; the outputs equal the
+    stream-synchronised call's (F110QP_SIG_POLL=0) bit for bit."""
+    import json
+    import os
+    from conftest import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "stiff_gap_n48_dt005.npz"))
+    src = str(d["source"])
+    knob("F110QP_GAP_SCREEN", screen)
+    over = json.loads(str(d["params"]))
+    import torch
+    N2, B = int(d["horizon"]), d["x0"].shape[0]
+    t = {k: torch.from_numpy(np.ascontiguousarray(d[k])).cuda() for k in ("x0", "u_lin", "x_ref", "halfspace")}
+    res = {}
+    for poll in ("1", "0"):
+        knob("F110QP_SIG_POLL", poll)
+        s = capi.Solver(capi.default_config(N2, gap_mode=capi.GAP_ACTIVE, **over))
+        o = _dev_outputs(torch, B, N2)
+        torch.cuda.synchronize()
+        s.prepare_dev(t["x0"], t["u_lin"], t["x_ref"], t["halfspace"], *o, stream=torch.cuda.Stream(), sync=True)()
+        res[poll] = [v.cpu().numpy() for v in o]  # read on the default stream
+        res[poll + "n"] = (s.sync_signals(), s.last_recheck_count())
+        s.close()
+    for p, q in zip(res["1"], res["0"]):
+        np.testing.assert_array_equal(p, q)
+    np.testing.assert_array_equal(res["1"][2], d["status"])
+    assert res["1n"][0] == 1 and res["0n"][0] == 0 and res["1n"][1] > 0, (res["1n"], res["0n"], src)
 
 
 def test_destroy_right_after_a_polled_call(capi):
