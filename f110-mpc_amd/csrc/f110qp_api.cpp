@@ -195,34 +195,26 @@ static int arm_signal(f110qp_ctx* c, int batch, int backend, const float* h, con
 }
 
 // Waits for the call armed by arm_signal (or synchronises the stream when it was not armed). The
-// poll reads only the word for its first 200 us (a hipStreamQuery inside the usual 10-15 us wait
-// delayed the answer by its own cost); from then on it asks the stream every 256 reads, so a
-// kernel that faults (no word) is reported by its HIP error, and a drained stream without the word
-// is reported as an error, not waited on.
+// poll reads only the word (a hipStreamQuery inside the usual 10-15 us wait delayed the answer by
+// its own cost and made the call bimodal); after 200 us it hands over to hipStreamSynchronize, so
+// a long call does not keep a core spinning and a kernel that faults (no word) is reported by its
+// HIP error. A drained stream without the word is an error, not a wait.
 static int wait_done(f110qp_ctx* c, hipStream_t s, bool armed) {
-  if (!armed) {
-    const hipError_t e = hipStreamSynchronize(s);
-    return e == hipSuccess ? F110QP_OK : hip_fail(e, "hipStreamSynchronize");
-  }
-  const unsigned seq = c->sig_seq;
-  const unsigned* w = (const unsigned*)c->hsig.p;
-  const auto t0 = std::chrono::steady_clock::now();
-  bool query = false;
-  for (unsigned k = 1;; k++) {
-    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return F110QP_OK;
-    if ((k & 255u) == 0) {
-      if (!query) query = std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200);
-      if (query) {
-        const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess) {
-          if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return F110QP_OK;
-          return fail(F110QP_ERR_HIP, "solve kernel finished without its completion signal");
-        }
-        if (q != hipErrorNotReady) return hip_fail(q, "hipStreamQuery");
-      }
+  if (armed) {
+    const unsigned seq = c->sig_seq;
+    const unsigned* w = (const unsigned*)c->hsig.p;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned k = 1;; k++) {
+      if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return F110QP_OK;
+      if ((k & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+      __builtin_ia32_pause();
     }
-    __builtin_ia32_pause();
   }
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  if (armed && __atomic_load_n((const unsigned*)c->hsig.p, __ATOMIC_ACQUIRE) != c->sig_seq)
+    return fail(F110QP_ERR_HIP, "solve kernel finished without its completion signal");
+  return F110QP_OK;
 }
 
 extern "C" {
