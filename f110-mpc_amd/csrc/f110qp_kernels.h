@@ -119,17 +119,40 @@ struct ObjOut {
   // (count + list; null: the re-check flags them itself)
   int* rc_count = nullptr;
   int* rc_list = nullptr;
-  // completion signal of a synchronous call (segmented lane kernel only, launch_signals): every
-  // wave arrives on sig_count once its stores are visible at system scope; the last one re-zeroes
-  // the count and writes sig_seq to sig_host (pinned host word the calling thread polls). null: none
+  // completion signal of a synchronous call, raised by its last kernel (signal_call_done): every
+  // workgroup arrives on sig_count once its stores are visible at system scope; the last one
+  // re-zeroes the count and writes sig_seq to sig_host (the pinned host word the calling thread
+  // polls). null: none
   unsigned* sig_host = nullptr;
   unsigned* sig_count = nullptr;
   unsigned sig_seq = 0;
 };
 
-// whether launch_solve's kernels for this call raise ObjOut's completion signal (the box-only solve
-// on the segmented lane kernel: one kernel per call); the caller synchronises the stream otherwise
+// whether launch_solve's kernels for this call raise ObjOut's completion signal (every ungrouped
+// call: its last kernel is a lane, wave or re-check kernel that signals); the caller synchronises
+// the stream otherwise
 bool launch_signals(const KParams& P, int B, int backend, const float* hs, const LaneWork& lw);
+
+// The completion signal at the very end of a call's last kernel (ObjOut::sig_*): every wave's
+// stores visible at system scope (zero-copy outputs in pinned host memory; device outputs written
+// back from this XCD's L2), then one arrival per workgroup (after a barrier when it has several
+// waves); the last arrival re-zeroes the count for the next call and publishes the call's number
+// to the host word the caller polls (f110qp_api.cpp wait_done). Every workgroup must reach it.
+__device__ __forceinline__ void signal_call_done(const ObjOut& oo) {
+  if (!oo.sig_host) return;
+  __threadfence_system();
+  if (blockDim.x > 64) __syncthreads();
+  if (threadIdx.x != 0) return;
+  if (gridDim.x == 1) {  // one workgroup: no arrival count to go through
+    __hip_atomic_store(oo.sig_host, oo.sig_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  const unsigned arrived = __hip_atomic_fetch_add(oo.sig_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (arrived + 1u == gridDim.x) {
+    __hip_atomic_store(oo.sig_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(oo.sig_host, oo.sig_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 
 // waves the lane kernel's grid aims for (one per CU of the MI355X's 256)
 constexpr int kLaneTargetWaves = 256;

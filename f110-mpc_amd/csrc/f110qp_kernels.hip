@@ -131,9 +131,10 @@ __global__ __launch_bounds__(256) void list_all_kernel(const int B, int* __restr
 }
 
 bool launch_signals(const KParams& P, int B, int backend, const float* hs, const LaneWork& lw) {
-  // gap rows: the call's last kernel is the fp64 re-check (launch_gap_recheck), which signals; box
-  // rows: the segmented lane kernel when it is the call's only kernel
-  return B > 0 && (hs != nullptr || (backend == BACKEND_LANE && lane_segments(P, B, lw) > 1));
+  // gap rows: the call's last kernel is the fp64 re-check (launch_gap_recheck); box rows: the one
+  // lane (sequential or segmented) or wave kernel of the call. Each signals from its last arrival.
+  (void)P; (void)backend; (void)hs; (void)lw;
+  return B > 0;
 }
 
 hipError_t launch_solve(const KParams& P, int B, const float* x0, const float* ul,

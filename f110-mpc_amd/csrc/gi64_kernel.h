@@ -752,21 +752,7 @@ __global__ __launch_bounds__(64 * ((2 * NUM + 63) / 64)) void gi64_kernel(const 
     gi64_qp<NUM>(sm, b, P, x0g, ulg, xrg, hsg, uout, xout, status_out, iters_out, oo);
     __syncthreads();
   }
-  if (oo.sig_host) {
-    // completion signal of a synchronous gap-row call (this launch is its last kernel; f110qp_api.cpp
-    // wait_done): every wave's stores visible at system scope, then one arrival per workgroup; the
-    // last one re-zeroes the count and publishes the call's number
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned arrived =
-          __hip_atomic_fetch_add(oo.sig_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (arrived + 1u == gridDim.x) {
-        __hip_atomic_store(oo.sig_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(oo.sig_host, oo.sig_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-  }
+  signal_call_done(oo);  // the completion word of a synchronous gap-row call (its last kernel)
 }
 
 template <int NUM>

@@ -746,6 +746,7 @@ __global__ __launch_bounds__(64) F110QP_LANE_ATTR void lane_kernel(const KParams
     o[5] = npass; o[6] = __builtin_amdgcn_s_memtime() - t_start; o[7] = 0;
   }
 #endif
+  signal_call_done(oo);  // a synchronous call's completion word (f110qp_kernels.h)
 }
 
 template <typename ST, bool SLDS, int L, bool ROT, bool DREF>

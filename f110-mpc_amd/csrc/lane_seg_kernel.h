@@ -854,23 +854,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     o[8] = t_stg - t_start; o[9] = t_lin - t_stg; o[10] = t_conv - t_lin; o[11] = t_setup - (t_conv - t_start);
   }
 #endif
-  if (oo.sig_host) {
-    // completion signal of a synchronous call (f110qp_api.cpp wait_done): the wave's stores
-    // visible at system scope (zero-copy outputs in pinned host memory; device outputs written
-    // back from this XCD's L2), then it arrives; the last wave re-zeroes the count for the next
-    // call and publishes the call's number to the host word the caller polls
-    __threadfence_system();
-    if (gridDim.x == 1) {  // one wave (up to 8 QPs at N = 20): no arrival count to go through
-      if (lane == 0) __hip_atomic_store(oo.sig_host, oo.sig_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else if (lane == 0) {
-      const unsigned arrived =
-          __hip_atomic_fetch_add(oo.sig_count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (arrived + 1u == gridDim.x) {
-        __hip_atomic_store(oo.sig_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(oo.sig_host, oo.sig_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-  }
+  signal_call_done(oo);  // a synchronous call's completion word (f110qp_kernels.h)
 }
 
 // Scratch of the segmented kernel for a batch: 1 fp64 (the lam-gains kept when they fit), 2 fp32

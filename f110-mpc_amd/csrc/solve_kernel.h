@@ -2374,6 +2374,7 @@ __global__ __launch_bounds__(64) F110QP_SOLVE_ATTR void solve_kernel(const KPara
                        gdbg, ws, oo);
     wsync();
   }
+  signal_call_done(oo);  // a synchronous box-only call's completion word (f110qp_kernels.h)
 }
 
 // Grouped mode, prepare launch: one wave per group builds the closed-form Hessian and the swept

@@ -180,8 +180,8 @@ void f110qp_destroy(f110qp_ctx* ctx);
  * MPC::Update's Linearize + gradient/constraint/bound updates + solver_.solve() +
  * getSolution (src/mpc.cpp:69-143) and UpdateSolvedTrajectory (src/mpc.cpp:145-159).
  * Up to 64 QPs the kernel reads the inputs from and writes the outputs to pinned host staging
- * (zero-copy), and the call returns on its kernels' completion word (f110qp_sync_signals) unless
- * it runs the sequential lane kernel; larger batches are staged through device memory. */
+ * (zero-copy), and the call returns on its last kernel's completion word (f110qp_sync_signals);
+ * larger batches are staged through device memory and wait for the stream. */
 int f110qp_solve_batch(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
                        const float* x_ref, const float* halfspace, float* u_out, float* x_out,
                        int* status, int* iters);
@@ -193,12 +193,10 @@ int f110qp_solve_batch_dev(f110qp_ctx* ctx, int batch, const float* x0, const fl
 
 /* f110qp_solve_batch_dev, then a wait until the results are in device memory: one call per
  * control tick for a caller that needs the answer before it returns, as solver_.solve() +
- * getSolution do in MPC::Update (src/mpc.cpp:133-142). A box-only call on the partitioned-horizon
- * lane kernel, and every gap-row call (whose last kernel is the fp64 re-check), waits on the
- * completion word that kernel's last wave or workgroup writes after a system-scope fence (the
- * outputs are then visible to any stream and to the host); the other calls (the sequential lane
- * kernel, the wave kernel's box path) synchronise `stream`. The kernel may still be retiring on
- * `stream` when this returns. */
+ * getSolution do in MPC::Update (src/mpc.cpp:133-142). The call waits on the completion word that
+ * its last kernel (lane or wave kernel; for gap rows the fp64 re-check) writes from its last wave
+ * or workgroup after a system-scope fence: the outputs are then visible to any stream and to the
+ * host. The kernel may still be retiring on `stream` when this returns. */
 int f110qp_solve_batch_dev_sync(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
                                 const float* x_ref, const float* halfspace, float* u_out,
                                 float* x_out, int* status, int* iters, void* stream);
@@ -299,10 +297,10 @@ int f110qp_last_recheck_count(f110qp_ctx* ctx, int* count);
 
 /* How many synchronous calls on this context (f110qp_solve_batch_dev_sync, and the host-pointer
  * calls of at most 64 QPs, whose kernel stores the outputs into pinned host memory) waited on the
- * kernel's completion word instead of synchronising the stream: the box-only solves on the
- * segmented lane kernel and the gap-row calls, whose last kernel (the segmented kernel, the fp64
- * re-check) publishes the call's number to a pinned host word after a system-scope fence
- * (single-QP latency). Other calls synchronise the stream. */
+ * kernel's completion word instead of synchronising the stream: every such call, whose last kernel
+ * (lane or wave kernel, for gap rows the fp64 re-check) publishes the call's number to a pinned
+ * host word after a system-scope fence (single-QP latency). Host-pointer calls of more
+ * than 64 QPs and the grouped calls synchronise the stream. */
 int f110qp_sync_signals(f110qp_ctx* ctx, unsigned* count);
 
 /* 1 for the test / measurement build (lib_test/libf110qp.so, -DF110QP_TEST_HOOKS), whose

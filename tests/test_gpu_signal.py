@@ -1,11 +1,11 @@
-"""Completion word of the synchronous calls (f110qp_api.cpp arm_signal / wait_done, lane_seg_kernel.h
-end): f110qp_solve_batch_dev_sync and the zero-copy host-pointer calls (<= 64 QPs) of a box-only
-solve on the segmented lane kernel return when the kernel's last wave has published the call's
-number to a pinned host word, not after hipStreamSynchronize. The outputs must then be complete:
+"""Completion word of the synchronous calls (f110qp_api.cpp arm_signal / wait_done, signal_call_done
+in f110qp_kernels.h): f110qp_solve_batch_dev_sync and the zero-copy host-pointer calls (<= 64 QPs)
+return when the call's last kernel has published the call's number to a pinned host word, not
+after hipStreamSynchronize. The outputs must then be complete:
 read back on ANOTHER stream with no dependency on the solve's, and equal, bit for bit, to the
 same calls waiting on the stream (the test build's F110QP_SIG_POLL=0) and to the asynchronous entry
-point. Calls whose work is several kernels (gap rows) or the sequential lane kernel (S = 1) are not
-armed and keep the stream synchronisation."""
+point. Every ungrouped call is armed: its last kernel (lane, wave or the gap rows' fp64 re-check)
+raises the signal; grouped calls and staged host calls (> 64 QPs) synchronise the stream."""
 import numpy as np
 import pytest
 
@@ -132,38 +132,42 @@ def test_signal_across_streams_and_entry_points(capi):
     fresh.close()
 
 
-def test_gap_calls_signal_from_the_recheck_and_sequential_calls_are_not_armed(capi, knob):
-    """Gap rows (lane screen or not, GI, then the fp64 re-check: several kernels) are armed, and the
-    re-check kernel, the call's last, raises the signal from its last workgroup; the sequential lane
-    kernel (F110QP_LANE_SEG=1) is not armed and synchronises the stream. Either way the answers equal
-    the asynchronous entry point's, on the device and through host pointers."""
+@pytest.mark.parametrize("backend", ["seq", "wave", "gap"])
+def test_every_ungrouped_call_signals_from_its_last_kernel(capi, knob, backend):
+    """The sequential lane kernel (F110QP_LANE_SEG=1), the wave kernel's box path and a gap-row call
+    (lane screen or not, GI, then the fp64 re-check: the last kernel signals from its last
+    workgroup) all answer synchronous calls through the completion word; the answers equal the
+    asynchronous entry point's, on the device and through host pointers."""
     import torch
     B = 64
-    knob("F110QP_LANE_SEG", 1)
-    seq = capi.Solver(capi.default_config(N))
-    assert seq.lane_segments(B) == 1
-    knob("F110QP_LANE_SEG", 0)
-    gap = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE))
+    if backend == "seq":
+        knob("F110QP_LANE_SEG", 1)
+        s = capi.Solver(capi.default_config(N, backend=capi.BACKEND_LANE))
+        assert s.lane_segments(B) == 1
+    elif backend == "wave":
+        s = capi.Solver(capi.default_config(N, backend=capi.BACKEND_WAVE))
+    else:
+        s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE))
     w = workload.make_batch(B, N, seed=41)
     hs = np.zeros((B, 2, 3), np.float32)
     hs[:, :, 2] = 1.0  # 0 x + 0 y >= -1: rows that never bind
     d = _dev_inputs(torch, w)
-    dh = torch.from_numpy(hs).cuda()
-    for s, h, armed in ((seq, None, 0), (gap, dh, 2)):
-        o1, o2 = _dev_outputs(torch, B, N), _dev_outputs(torch, B, N)
-        s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], h, *o1, sync=True)()
-        r1 = [t.cpu().numpy() for t in o1]
-        s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], h, *o2)()
-        torch.cuda.synchronize()
-        r2 = [t.cpu().numpy() for t in o2]
-        for p, q in zip(r1, r2):
-            np.testing.assert_array_equal(p, q)
-        assert (r1[2] == capi.SOLVED).all()
-        u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs if h is not None else None)
-        np.testing.assert_array_equal(u, r1[0])
-        assert s.sync_signals() == armed
-    seq.close()
-    gap.close()
+    h = torch.from_numpy(hs).cuda() if backend == "gap" else None
+    o1, o2 = _dev_outputs(torch, B, N), _dev_outputs(torch, B, N)
+    side = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], h, *o1, stream=side, sync=True)()
+    r1 = [t.cpu().numpy() for t in o1]  # read on the default stream
+    s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], h, *o2)()
+    torch.cuda.synchronize()
+    r2 = [t.cpu().numpy() for t in o2]
+    for p, q in zip(r1, r2):
+        np.testing.assert_array_equal(p, q)
+    assert (r1[2] == capi.SOLVED).all()
+    u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"], hs if h is not None else None)
+    np.testing.assert_array_equal(u, r1[0])
+    assert s.sync_signals() == 2
+    s.close()
 
 
 @pytest.mark.parametrize("screen", ["0", "1"])
