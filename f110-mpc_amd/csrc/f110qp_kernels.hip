@@ -84,8 +84,19 @@ __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int*
   __shared__ int off[2][kPrioMax + 1];
   const int t = threadIdx.x;
   if (t <= kPrioMax) hist[t] = 0;
+  // the first kHold x 1,024 priorities stay in registers for the scatter (one global read of them)
+  constexpr int kHold = 8;
+  int held[kHold];
+#pragma unroll
+  for (int k = 0; k < kHold; k++) {
+    const int b = t + 1024 * k;
+    held[k] = b < B ? min(prio[b], kPrioMax) : 0;
+  }
   __syncthreads();
-  for (int b = t; b < B; b += 1024) {
+#pragma unroll
+  for (int k = 0; k < kHold; k++)
+    if (held[k] > 0) atomicAdd(&hist[held[k]], 1);
+  for (int b = t + 1024 * kHold; b < B; b += 1024) {
     const int p = min(prio[b], kPrioMax);
     if (p > 0) atomicAdd(&hist[p], 1);
   }
@@ -116,7 +127,10 @@ __global__ __launch_bounds__(1024) void gap_order_kernel(const int B, const int*
   // i.e. the inclusive prefix at scan index kPrioMax - p - 1 (0 for the top priority)
   if (t >= 1 && t <= kPrioMax) off[0][t] = (t >= 2) ? hist[t - 2] : 0;
   __syncthreads();
-  for (int b = t; b < B; b += 1024) {
+#pragma unroll
+  for (int k = 0; k < kHold; k++)
+    if (held[k] > 0) list[atomicAdd(&off[0][kPrioMax + 1 - held[k]], 1)] = t + 1024 * k;
+  for (int b = t + 1024 * kHold; b < B; b += 1024) {
     const int p = min(prio[b], kPrioMax);
     if (p > 0) list[atomicAdd(&off[0][kPrioMax + 1 - p], 1)] = b;
   }
