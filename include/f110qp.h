@@ -193,10 +193,11 @@ int f110qp_solve_batch_dev(f110qp_ctx* ctx, int batch, const float* x0, const fl
 
 /* f110qp_solve_batch_dev, then a wait until the results are in device memory: one call per
  * control tick for a caller that needs the answer before it returns, as solver_.solve() +
- * getSolution do in MPC::Update (src/mpc.cpp:133-142). The call waits on the completion word that
- * its last kernel (lane or wave kernel; for gap rows the fp64 re-check) writes from its last wave
- * or workgroup after a system-scope fence: the outputs are then visible to any stream and to the
- * host. The kernel may still be retiring on `stream` when this returns. */
+ * getSolution do in MPC::Update (src/mpc.cpp:133-142). When the call's last kernel (lane or wave
+ * kernel; for gap rows the fp64 re-check) has at most 256 workgroups, the call waits on the
+ * completion word that kernel writes from its last wave or workgroup after a system-scope fence:
+ * the outputs are then visible to any stream and to the host, and the kernel may still be retiring
+ * on `stream` when this returns. Larger launches synchronise `stream`. */
 int f110qp_solve_batch_dev_sync(f110qp_ctx* ctx, int batch, const float* x0, const float* u_lin,
                                 const float* x_ref, const float* halfspace, float* u_out,
                                 float* x_out, int* status, int* iters, void* stream);
@@ -297,10 +298,11 @@ int f110qp_last_recheck_count(f110qp_ctx* ctx, int* count);
 
 /* How many synchronous calls on this context (f110qp_solve_batch_dev_sync, and the host-pointer
  * calls of at most 64 QPs, whose kernel stores the outputs into pinned host memory) waited on the
- * kernel's completion word instead of synchronising the stream: every such call, whose last kernel
- * (lane or wave kernel, for gap rows the fp64 re-check) publishes the call's number to a pinned
- * host word after a system-scope fence (single-QP latency). Host-pointer calls of more
- * than 64 QPs and the grouped calls synchronise the stream. */
+ * kernel's completion word instead of synchronising the stream: the calls whose last kernel (lane or
+ * wave kernel, for gap rows the fp64 re-check) has at most 256 workgroups, which publishes the
+ * call's number to a pinned host word after a system-scope fence (single-QP latency).
+ * Larger launches, host-pointer calls of more than 64 QPs and the grouped calls synchronise the
+ * stream. */
 int f110qp_sync_signals(f110qp_ctx* ctx, unsigned* count);
 
 /* 1 for the test / measurement build (lib_test/libf110qp.so, -DF110QP_TEST_HOOKS), whose

@@ -1,0 +1,50 @@
+"""Synchronous call cost at large batches: f110qp_solve_batch_dev_sync (the completion word: every
+wave's system-scope fence, then one arrival each) against the asynchronous call plus a stream
+synchronize, per batch size (kernel work identical). Prints one JSON line per size.
+
+    python tools/sync_batch_probe.py
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "f110-mpc_amd"))
+
+
+def main():
+    import torch
+
+    from f110qp import capi, workload
+
+    for N, B in ((20, 1024), (20, 4096), (20, 65536), (40, 8192), (40, 65536)):
+        w = workload.make_batch(B, N, seed=3)
+        d = {k: torch.from_numpy(np.ascontiguousarray(w[k])).cuda() for k in ("x0", "u_lin", "x_ref")}
+        o = (torch.empty((B, N, 2), device="cuda"), torch.empty((B, N + 1, 3), device="cuda"),
+             torch.empty((B,), dtype=torch.int32, device="cuda"))
+        st = torch.cuda.Stream()
+        s = capi.Solver(capi.default_config(N))
+        fs = s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], None, *o, stream=st, sync=True)
+        fa = s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], None, *o, stream=st)
+        for _ in range(10):
+            fs()
+        ts, ta = [], []
+        for i in range(60):
+            t0 = time.perf_counter()
+            fs()
+            ts.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            fa()
+            st.synchronize()
+            ta.append(time.perf_counter() - t0)
+        print(json.dumps({"N": N, "B": B, "dev_sync_p50_us": round(float(np.median(ts)) * 1e6, 1),
+                          "async_then_sync_p50_us": round(float(np.median(ta)) * 1e6, 1),
+                          "polled": s.sync_signals()}), flush=True)
+        s.close()
+
+
+if __name__ == "__main__":
+    main()
