@@ -196,9 +196,11 @@ static int arm_signal(f110qp_ctx* c, int batch, int backend, const float* h, con
 
 // Waits for the call armed by arm_signal (or synchronises the stream when it was not armed). The
 // poll reads only the word (a hipStreamQuery inside the usual 10-15 us wait delayed the answer by
-// its own cost and made the call bimodal); after 200 us it hands over to hipStreamSynchronize, so
-// a long call does not keep a core spinning and a kernel that faults (no word) is reported by its
-// HIP error. A drained stream without the word is an error, not a wait.
+// its own cost and made the call bimodal); after kPollWindow it hands over to hipStreamSynchronize,
+// so a stalled call does not keep a core spinning and a kernel that faults (no word) is reported by
+// its HIP error (a gap-row call of 256 QPs, ~245 us, lost 7 us when the hand-over came at 200 us).
+// A drained stream without the word is an error, not a wait.
+constexpr auto kPollWindow = std::chrono::microseconds(1000);
 static int wait_done(f110qp_ctx* c, hipStream_t s, bool armed) {
   if (armed) {
     const unsigned seq = c->sig_seq;
@@ -206,7 +208,7 @@ static int wait_done(f110qp_ctx* c, hipStream_t s, bool armed) {
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned k = 1;; k++) {
       if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) return F110QP_OK;
-      if ((k & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+      if ((k & 255u) == 0 && std::chrono::steady_clock::now() - t0 > kPollWindow) break;
       __builtin_ia32_pause();
     }
   }

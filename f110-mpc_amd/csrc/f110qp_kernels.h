@@ -137,10 +137,12 @@ bool launch_signals(const KParams& P, int B, int backend, const float* hs, const
 // stores visible at system scope (zero-copy outputs in pinned host memory; device outputs written
 // back from this XCD's L2), then one arrival per workgroup (after a barrier when it has several
 // waves); the last arrival re-zeroes the count for the next call and publishes the call's number
-// to the host word the caller polls (f110qp_api.cpp wait_done). Every workgroup must reach it.
-__device__ __forceinline__ void signal_call_done(const ObjOut& oo) {
+// to the host word the caller polls (f110qp_api.cpp wait_done). Every workgroup must reach it; one
+// that stored nothing (wrote = false: a re-check workgroup past the list) skips the fence, whose L2
+// write-back walk is what makes a burst of them costly.
+__device__ __forceinline__ void signal_call_done(const ObjOut& oo, bool wrote = true) {
   if (!oo.sig_host) return;
-  __threadfence_system();
+  if (wrote) __threadfence_system();
   if (blockDim.x > 64) __syncthreads();
   if (threadIdx.x != 0) return;
   if (gridDim.x == 1) {  // one workgroup: no arrival count to go through

@@ -752,7 +752,7 @@ __global__ __launch_bounds__(64 * ((2 * NUM + 63) / 64)) void gi64_kernel(const 
     gi64_qp<NUM>(sm, b, P, x0g, ulg, xrg, hsg, uout, xout, status_out, iters_out, oo);
     __syncthreads();
   }
-  signal_call_done(oo);  // the completion word of a synchronous gap-row call (its last kernel)
+  signal_call_done(oo, (int)blockIdx.x < n);  // the completion word of a synchronous gap-row call
 }
 
 template <int NUM>

@@ -20,15 +20,22 @@ def main():
 
     from f110qp import capi, workload
 
-    for N, B in ((20, 1024), (20, 4096), (20, 65536), (40, 8192), (40, 65536)):
-        w = workload.make_batch(B, N, seed=3)
+    for N, B, gap in ((20, 1024, False), (20, 4096, False), (20, 65536, False), (40, 8192, False),
+                      (40, 65536, False), (20, 1, True), (20, 256, True), (20, 4096, True)):
+        w = workload.make_batch(B, N, seed=1000)
         d = {k: torch.from_numpy(np.ascontiguousarray(w[k])).cuda() for k in ("x0", "u_lin", "x_ref")}
         o = (torch.empty((B, N, 2), device="cuda"), torch.empty((B, N + 1, 3), device="cuda"),
              torch.empty((B,), dtype=torch.int32, device="cuda"))
         st = torch.cuda.Stream()
-        s = capi.Solver(capi.default_config(N))
-        fs = s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], None, *o, stream=st, sync=True)
-        fa = s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], None, *o, stream=st)
+        hs = None
+        if gap:  # the C3 half-spaces: one scan per QP through the device FindHalfSpaces
+            ranges, amin, ainc, amax = workload.make_scans(B, seed=2000)
+            hs = torch.empty((B, 2, 3), dtype=torch.float32, device="cuda")
+            capi.find_half_spaces_dev(d["x0"], torch.from_numpy(ranges).cuda(), amin, ainc, amax, hs)
+            torch.cuda.synchronize()
+        s = capi.Solver(capi.default_config(N, gap_mode=capi.GAP_ACTIVE if gap else capi.GAP_INACTIVE))
+        fs = s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], hs, *o, stream=st, sync=True)
+        fa = s.prepare_dev(d["x0"], d["u_lin"], d["x_ref"], hs, *o, stream=st)
         for _ in range(10):
             fs()
         ts, ta = [], []
@@ -40,7 +47,7 @@ def main():
             fa()
             st.synchronize()
             ta.append(time.perf_counter() - t0)
-        print(json.dumps({"N": N, "B": B, "dev_sync_p50_us": round(float(np.median(ts)) * 1e6, 1),
+        print(json.dumps({"N": N, "B": B, "gap": gap, "dev_sync_p50_us": round(float(np.median(ts)) * 1e6, 1),
                           "async_then_sync_p50_us": round(float(np.median(ta)) * 1e6, 1),
                           "polled": s.sync_signals()}), flush=True)
         s.close()
