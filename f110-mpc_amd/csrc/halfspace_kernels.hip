@@ -69,21 +69,23 @@ __global__ __launch_bounds__(256) void half_space_kernel(int B, const float* __r
   float v[kHsBatch];  // the last batch of blocks stays in registers for the tail
 #pragma unroll
   for (int j = 0; j < kHsBatch; j++) v[j] = 0.f;
+  const unsigned last = (unsigned)(num_scans - 1);
   for (int k0 = 0; k0 < nblk; k0 += kHsBatch) {
+    // unconditional loads (clamped index): no exec masking; a 32-bit offset from the scan's
+    // wave-uniform base (one min and one shift per load)
 #pragma unroll
-    for (int j = 0; j < kHsBatch; j++) {  // unconditional loads (clamped index): no exec masking
-      const int p = 64 * (k0 + j) + lane;
-      v[j] = r[p < num_scans ? p : num_scans - 1];
-    }
+    for (int j = 0; j < kHsBatch; j++) v[j] = r[min((unsigned)(64 * (k0 + j) + lane), last)];
+    // fully unrolled (a wave-uniform guard per block instead of a break: the break kept the loop
+    // rolled, v[j] then went through dynamic register indexing)
 #pragma unroll
     for (int j = 0; j < kHsBatch; j++) {
       const int k = k0 + j;
-      if (k >= nblk) break;
+      if (k >= nblk) continue;
       const int p = 64 * k + lane;
       const float angle = angle_min + (float)p * angle_inc;  // :133
       const bool inwin = p < num_scans && angle > -lim && angle < lim;
       const bool open = inwin && v[j] > thresh;  // :138
-      const unsigned long long W = __ballot(inwin), M = __ballot(open);
+      const unsigned long long W = __builtin_amdgcn_ballot_w64(inwin), M = __builtin_amdgcn_ballot_w64(open);
       if (w0 < 0 && W) {
         const int t = __builtin_ctzll(W);
         w0 = 64 * k + t;

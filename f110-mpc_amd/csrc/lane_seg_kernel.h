@@ -51,7 +51,7 @@ namespace f110qp {
 // Diagnostic build only (-DF110QP_STAMPS on lane_seg_inst.hip): per-wave cycles of the setup, each
 // pass phase and the output, read back with f110qp_read_seg_stamps(). Never in the shipped library.
 #ifdef F110QP_STAMPS
-constexpr int kSegStampSlots = 12;
+constexpr int kSegStampSlots = 16;
 __device__ unsigned long long g_sstamps[4096 * kSegStampSlots];
 #define SSTAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #define SACC(acc, since) acc += __builtin_amdgcn_s_memtime() - (since)
@@ -169,6 +169,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   SSTAMP(t_start);
 #ifdef F110QP_STAMPS
   unsigned long long acc_bw = 0, acc_dual = 0, acc_ref = 0, acc_fw = 0, t_setup = 0, npass = 0;
+  unsigned long long t_out_loop = 0;  // the output sweep's stage loop
 #endif
   constexpr bool F32 = sizeof(ST) == 4;
   char* const lbase = reinterpret_cast<char*>(seg_smem);
@@ -289,6 +290,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   const double rNx = __shfl(r64[(3 * (m - 1) + 0) * 64], lane | (S - 1));
   const double rNy = __shfl(r64[(3 * (m - 1) + 1) * 64], lane | (S - 1));
   const double rNt = __shfl(r64[(3 * (m - 1) + 2) * 64], lane | (S - 1));
+  SSTAMP(t_rn);
 
   // warm start: previous tick's active bounds when the slot's (theta0, v, steer) bits repeat
   const int R = (2 * N + 63) / 64;
@@ -336,6 +338,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       ap[t * 64] = (tw && 2 * (s0 + t) < N) ? sv : a;
     }
   }
+  SSTAMP(t_mask);
 
   // whether any of the lane's QP's S lanes has its bit set in a ballot
   auto qany = [&](unsigned long long mk) { return ((mk >> (sl * S)) & ((1ull << S) - 1ull)) != 0ull; };
@@ -451,10 +454,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         const double W20 = ROT ? F20 * b00 + F22 * b20 : F20 * b00 + F21 * b10 + F22 * b20;
         const double W01 = F02 * b21, W11 = F12 * b21, W21 = F22 * b21;
         // lam-gain of u_i: Fl = -S^-1 W'
-        const double L00 = -(I00 * W00 + I01 * W01), L01 = -(I00 * W10 + I01 * W11);
-        const double L02 = -(I00 * W20 + I01 * W21);
-        const double L10 = -(I01 * W00 + I11 * W01), L11 = -(I01 * W10 + I11 * W11);
-        const double L12 = -(I01 * W20 + I11 * W21);
+        // (written as -a b - c d: the negation folds into the fma's source modifiers, where
+        // -(a b + c d) cost a v_xor per entry)
+        const double L00 = -I00 * W00 - I01 * W01, L01 = -I00 * W10 - I01 * W11;
+        const double L02 = -I00 * W20 - I01 * W21;
+        const double L10 = -I01 * W00 - I11 * W01, L11 = -I01 * W10 - I11 * W11;
+        const double L12 = -I01 * W20 - I11 * W21;
         if constexpr (FST) {
           s[8 * 64] = L00; s[9 * 64] = L01; s[10 * 64] = L02;
           s[11 * 64] = L10; s[12 * 64] = L11; s[13 * 64] = L12;
@@ -519,25 +524,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         double iz = __builtin_amdgcn_rcp(zdet);
         iz = fma(iz, fma(-zdet, iz, 1.0), iz);
         iz = fma(iz, fma(-zdet, iz, 1.0), iz);
-        // Mn Phi and Mn psi + mn
-        const double U00 = N00 * F00 + N01 * F10 + N02 * F20, U01 = N00 * F01 + N01 * F11 + N02 * F21;
-        const double U02 = N00 * F02 + N01 * F12 + N02 * F22;
-        const double U10 = N01 * F00 + N11 * F10 + N12 * F20, U11 = N01 * F01 + N11 * F11 + N12 * F21;
-        const double U12 = N01 * F02 + N11 * F12 + N12 * F22;
-        const double U20 = N02 * F00 + N12 * F10 + N22 * F20, U21 = N02 * F01 + N12 * F11 + N22 * F21;
-        const double U22 = N02 * F02 + N12 * F12 + N22 * F22;
-        const double u0 = N00 * s0v + N01 * s1v + N02 * s2v + n0;
-        const double u1 = N01 * s0v + N11 * s1v + N12 * s2v + n1;
-        const double u2 = N02 * s0v + N12 * s1v + N22 * s2v + n2;
-        T00 = iz * (A00 * U00 + A01 * U10 + A02 * U20); T01 = iz * (A00 * U01 + A01 * U11 + A02 * U21);
-        T02 = iz * (A00 * U02 + A01 * U12 + A02 * U22);
-        T10 = iz * (A10 * U00 + A11 * U10 + A12 * U20); T11 = iz * (A10 * U01 + A11 * U11 + A12 * U21);
-        T12 = iz * (A10 * U02 + A11 * U12 + A12 * U22);
-        T20 = iz * (A20 * U00 + A21 * U10 + A22 * U20); T21 = iz * (A20 * U01 + A21 * U11 + A22 * U21);
-        T22 = iz * (A20 * U02 + A21 * U12 + A22 * U22);
-        t0 = iz * (A00 * u0 + A01 * u1 + A02 * u2);
-        t1 = iz * (A10 * u0 + A11 * u1 + A12 * u2);
-        t2 = iz * (A20 * u0 + A21 * u1 + A22 * u2);
+        // Y = Z^-1 Mn is symmetric ((I - N G)^-1 N = N (I - G N)^-1 for symmetric N, G): six
+        // entries, then T = Y Phi and t = Y psi + Z^-1 mn (15 fewer fp64 operations per step than
+        // T = Z^-1 (Mn Phi))
+        const double Y00 = iz * (A00 * N00 + A01 * N01 + A02 * N02);
+        const double Y01 = iz * (A00 * N01 + A01 * N11 + A02 * N12);
+        const double Y02 = iz * (A00 * N02 + A01 * N12 + A02 * N22);
+        const double Y11 = iz * (A10 * N01 + A11 * N11 + A12 * N12);
+        const double Y12 = iz * (A10 * N02 + A11 * N12 + A12 * N22);
+        const double Y22 = iz * (A20 * N02 + A21 * N12 + A22 * N22);
+        T00 = Y00 * F00 + Y01 * F10 + Y02 * F20; T01 = Y00 * F01 + Y01 * F11 + Y02 * F21;
+        T02 = Y00 * F02 + Y01 * F12 + Y02 * F22;
+        T10 = Y01 * F00 + Y11 * F10 + Y12 * F20; T11 = Y01 * F01 + Y11 * F11 + Y12 * F21;
+        T12 = Y01 * F02 + Y11 * F12 + Y12 * F22;
+        T20 = Y02 * F00 + Y12 * F10 + Y22 * F20; T21 = Y02 * F01 + Y12 * F11 + Y22 * F21;
+        T22 = Y02 * F02 + Y12 * F12 + Y22 * F22;
+        const double an0 = A00 * n0 + A01 * n1 + A02 * n2, an1 = A10 * n0 + A11 * n1 + A12 * n2;
+        const double an2 = A20 * n0 + A21 * n1 + A22 * n2;
+        t0 = Y00 * s0v + Y01 * s1v + Y02 * s2v + iz * an0;
+        t1 = Y01 * s0v + Y11 * s1v + Y12 * s2v + iz * an1;
+        t2 = Y02 * s0v + Y12 * s1v + Y22 * s2v + iz * an2;
         // M = P + Phi' T, m = a + Phi' t
         M00 = P00 + F00 * T00 + F10 * T10 + F20 * T20;
         M01 = P01 + F00 * T01 + F10 * T11 + F20 * T21;
@@ -747,6 +753,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     ga0 = h6[0]; gb0 = h6[1]; gc0 = h6[2]; ga1 = h6[3]; gb1 = h6[4]; gc1 = h6[5];
   }
   int nviol = 0;  // gap rows of this lane's stages the box optimum violates (or within the margin)
+  SSTAMP(t_ol0);
   {
     double x0 = xs0, x1 = xs1, x2 = xs2;
     for (int t = 0; t < m; t++) {
@@ -786,6 +793,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     }
     if (want_obj && top) qterm(rNx, rNy, rNt, x0, x1, x2);  // x_N against x_ref[N-1]
   }
+  SACC(t_out_loop, t_ol0);
   if (want_obj) {
 #pragma unroll
     for (int k = 1; k < S; k <<= 1) {
@@ -852,6 +860,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     o[0] = t_setup; o[1] = acc_bw; o[2] = acc_dual; o[3] = acc_ref; o[4] = acc_fw;
     o[5] = t_end - t_out; o[6] = npass; o[7] = t_end - t_start;
     o[8] = t_stg - t_start; o[9] = t_lin - t_stg; o[10] = t_conv - t_lin; o[11] = t_setup - (t_conv - t_start);
+    o[12] = t_rn - t_conv; o[13] = t_mask - t_rn; o[14] = t_setup - (t_mask - t_start); o[15] = t_out_loop;
   }
 #endif
   signal_call_done(oo);  // a synchronous call's completion word (f110qp_kernels.h)

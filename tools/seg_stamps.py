@@ -24,7 +24,7 @@ S = s.lane_segments(B)
 for _ in range(3):
     u, x, st, it = s.solve(w["x0"], w["u_lin"], w["x_ref"])
 W = min(4096, (B * S + 63) // 64)
-buf = np.zeros((W, 12), np.uint64)
+buf = np.zeros((W, 16), np.uint64)
 L.f110qp_read_seg_stamps.argtypes = [C.c_void_p, C.c_int]
 L.f110qp_read_seg_stamps(C.c_void_p(buf.ctypes.data), W)
 b = buf.astype(float)
@@ -32,7 +32,8 @@ tot = b[:, 7]
 print(f"B={B} N={N} S={S} waves={W} passes per wave mean {b[:, 6].mean():.2f} max {b[:, 6].max():.0f}")
 for i, n in enumerate(["setup", "backward", "segment ends", "refresh", "forward", "output"]):
     print(f"{n:14s} mean {b[:, i].mean():8.0f}  max {b[:, i].max():8.0f}  share {b[:, i].mean() / tot.mean() * 100:5.1f}%")
-for i, n in zip(range(8, 12), ["  staging", "  linearize", "  refs to fp64", "  warm + rest"]):
+for i, n in zip(range(8, 16), ["  staging", "  linearize", "  refs to fp64", "  warm + rest", "    rN shfl",
+                                "    mask init", "    rest", "  out loop"]):
     print(f"{n:14s} mean {b[:, i].mean():8.0f}  max {b[:, i].max():8.0f}")
 np_ = np.maximum(b[:, 6], 1)
 print(f"per pass: backward {np.mean(b[:, 1] / np_):.0f}, segment ends {np.mean(b[:, 2] / np_):.0f}, refresh "
