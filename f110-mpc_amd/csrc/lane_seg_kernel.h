@@ -127,7 +127,7 @@ __device__ __forceinline__ double seg_dn(double v, int lane) {
 // neutral (tools/ab_seg_variant.sh)
 #define F110QP_SEG_WPE 2
 #endif
-template <int S, bool ROT, bool FST, typename ST = double, bool SCR = false, bool TWIN = false>
+template <int S, bool ROT, bool FST, typename ST = double, bool SCR = false, bool TWIN = false, bool EVEN = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_WPE, F110QP_SEG_WPE))) void lane_seg_kernel(
     const KParams P, const int B, const float* __restrict__ x0g, const float* __restrict__ ulg,
     const float* __restrict__ xrg, float* __restrict__ uout, float* __restrict__ xout,
@@ -160,10 +160,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   const int b = vq >> twin;
   const int N = P.N;
   // segments of q or q + 1 stages (the first N mod S ones longer); LDS rows for the longest
-  const int q = N / S, rem = N - q * S;
-  const int m = q + (seg < rem ? 1 : 0);
-  const int s0 = seg * q + (seg < rem ? seg : rem);
-  const int mM = q + (rem > 0 ? 1 : 0);
+  // EVEN (S divides N, the launcher's choice): every segment has q stages, so the stage loops run
+  // on a wave-uniform count (scalar loop control and LDS strides instead of per-lane ones)
+  const int q = N / S, rem = EVEN ? 0 : N - q * S;
+  const int m = EVEN ? q : q + (seg < rem ? 1 : 0);
+  const int s0 = EVEN ? seg * q : seg * q + (seg < rem ? seg : rem);
+  const int mM = EVEN ? q : q + (rem > 0 ? 1 : 0);
   const bool top = seg == S - 1;
 
   SSTAMP(t_start);
@@ -912,7 +914,7 @@ hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const flo
   // forces the refresh (test hook, F110QP_LANE_DREF=0)
   const size_t per_cu = ((size_t)waves + 255) / 256;
   const bool fst = mode == 1 && lw.dref && per_cu * seg_lds_bytes(P.N, S, true) <= 160 * 1024;
-  auto go = [&](auto kern, size_t lds) -> hipError_t {
+  auto go1 = [&](auto kern, size_t lds) -> hipError_t {
     if (lds > 64 * 1024) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -922,10 +924,15 @@ hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const flo
                        lw.kmax, oo);
     return hipGetLastError();
   };
-  if (twin) return go(&lane_seg_kernel<S, ROT, true, double, SCR, true>, seg_lds_bytes(P.N, S, true));
-  if (mode == 2) return go(&lane_seg_kernel<S, ROT, false, float, SCR>, seg_lds_bytes(P.N, S, false, true));
-  return fst ? go(&lane_seg_kernel<S, ROT, true, double, SCR>, seg_lds_bytes(P.N, S, true))
-             : go(&lane_seg_kernel<S, ROT, false, double, SCR>, seg_lds_bytes(P.N, S, false));
+  const bool even = P.N % S == 0;  // equal segments: the EVEN instantiation
+#define F110QP_SEG_GO(FST_, ST_, TWIN_, LDS_)                                              \
+  (even ? go1(&lane_seg_kernel<S, ROT, FST_, ST_, SCR, TWIN_, true>, LDS_)                 \
+        : go1(&lane_seg_kernel<S, ROT, FST_, ST_, SCR, TWIN_, false>, LDS_))
+  if (twin) return F110QP_SEG_GO(true, double, true, seg_lds_bytes(P.N, S, true));
+  if (mode == 2) return F110QP_SEG_GO(false, float, false, seg_lds_bytes(P.N, S, false, true));
+  return fst ? F110QP_SEG_GO(true, double, false, seg_lds_bytes(P.N, S, true))
+             : F110QP_SEG_GO(false, double, false, seg_lds_bytes(P.N, S, false));
+#undef F110QP_SEG_GO
 }
 
 }  // namespace f110qp
