@@ -16,9 +16,9 @@ hipError_t launch_lane_seg_t(const KParams& P, int B, const float* x0, const flo
                              float* uo, float* xo, int* st, int* its, const WarmState& ws,
                              const LaneWork& lw, const ObjOut& oo, hipStream_t s);  // lane_seg_inst.hip
 // LDS per wave of the segmented kernel with fp64 / fp32 references and scratch (lane_seg_kernel.h
-// seg_lds_bytes without the lam-gains)
+// seg_lds_bytes without the lam-gains, with its 1 KiB state-code tables: two with fp64 scratch)
 constexpr size_t seg_lds_per_wave(int N, int S, bool f32 = false) {
-  return (size_t)((N + S - 1) / S) * 64 * (3 * (f32 ? 4 : 8) + 4 + 11 * (f32 ? 4 : 8));
+  return (size_t)((N + S - 1) / S) * 64 * (3 * (f32 ? 4 : 8) + 4 + 11 * (f32 ? 4 : 8)) + (f32 ? 1 : 2) * 1024;
 }
 
 // Horizon segments per QP (lane_seg_kernel.h). A batch whose waves leave SIMDs idle (the QPs fit

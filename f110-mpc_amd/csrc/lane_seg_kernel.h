@@ -65,8 +65,12 @@ __device__ unsigned long long g_sstamps[4096 * kSegStampSlots];
 // FST: the scratch keeps the lam-gains F_i (6) instead of S_i^-1 (3): 14 doubles per stage
 // F32: references and Riccati scratch held as float (the fp64 arithmetic is unchanged): 60 instead
 // of 116 bytes per stage and lane, so 16,384 x N = 40 QPs per GPU fit at S = 4 (DESIGN.md 2b')
+// + the per-wave tables of the active-state codes (kSegTabBytes: the backward sweep's bound values
+// and free masks, the fp64-scratch forward sweep's re-guess thresholds, 16 codes x 8 doubles each)
+constexpr size_t kSegTabBytes = 16 * 8 * 8;
 constexpr size_t seg_lds_bytes(int N, int S, bool fst = false, bool f32 = false) {
-  return (size_t)((N + S - 1) / S) * 64 * (3 * (f32 ? 4 : 8) + 4 + (fst ? 14 : 11) * (f32 ? 4 : 8));
+  return (size_t)((N + S - 1) / S) * 64 * (3 * (f32 ? 4 : 8) + 4 + (fst ? 14 : 11) * (f32 ? 4 : 8)) +
+         (f32 ? 1 : 2) * kSegTabBytes;
 }
 
 template <int M>
@@ -179,6 +183,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   ST* const r64 = reinterpret_cast<ST*>(lbase) + lane;                     // [3mM][64]
   int* const ap = reinterpret_cast<int*>(lbase + o_ap) + lane;             // [mM][64]
   ST* const sc = reinterpret_cast<ST*>(lbase + o_sc) + lane;               // [mM][NV][64]
+  // code tables (wave-uniform base; a lane reads the entry of its own stage's state code)
+  double* const btab = reinterpret_cast<double*>(lbase + o_sc + (size_t)mM * NV * 64 * sizeof(ST));
+  double* const ftab = btab + 16 * 8;  // (ST = double only)
 
   // per-QP inputs and the warm-start traffic switch (warm_traffic), issued before the staging loads
   const float fX0 = x0g[3 * b + 0], fY0 = x0g[3 * b + 1], fTH0 = x0g[3 * b + 2];
@@ -284,6 +291,28 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       r64[(3 * t + 0) * 64] = ROT ? cs * dx + sn * dy : dx;
       r64[(3 * t + 1) * 64] = ROT ? cs * dy - sn * dx : dy;
       r64[(3 * t + 2) * 64] = (double)ft - th0;
+    }
+    // the active-state code tables: code c holds input a's state (c >> 2a) & 3 (0 free, 1 lower,
+    // 2 upper). btab[c] = (bA0, bA1, fm0, 1 - fm0, fm1, 1 - fm1, fm0 fm1, 0): the fixed inputs'
+    // bound values and the free masks of the masked 2 x 2 solve (products with 0 / 1 instead of
+    // ~20 selects per backward stage). ftab[c] = per input (u < t1, u > t2, g > t3, g < t4 tests):
+    // the free input's box with the re-guess tolerance, a bound's multiplier sign test, +-inf
+    // where the test does not apply (fp64 scratch: one set of tolerances for both pass kinds)
+    if (lane < 16) {
+      const int cA = lane & 3, cB = (lane >> 2) & 3;
+      const double fA = cA == 0 ? 1.0 : 0.0, fB = cB == 0 ? 1.0 : 0.0;
+      double* e = btab + 8 * lane;
+      e[0] = cA == 0 ? 0.0 : (cA == 1 ? lb0 : ub0);
+      e[1] = cB == 0 ? 0.0 : (cB == 1 ? lb1 : ub1);
+      e[2] = fA; e[3] = 1.0 - fA; e[4] = fB; e[5] = 1.0 - fB; e[6] = fA * fB; e[7] = 0.0;
+      if constexpr (!F32) {
+        const double inf = __builtin_inf();
+        double* f = ftab + 8 * lane;
+        f[0] = cA == 0 ? lbe0 : -inf; f[1] = cA == 0 ? ube0 : inf;
+        f[2] = cA == 1 ? -gtol0 : inf; f[3] = cA == 2 ? gtol0 : -inf;
+        f[4] = cB == 0 ? lbe1 : -inf; f[5] = cB == 0 ? ube1 : inf;
+        f[6] = cB == 1 ? -gtol1 : inf; f[7] = cB == 2 ? gtol1 : -inf;
+      }
     }
     __syncthreads();  // the staging region becomes the Riccati scratch
   }
@@ -419,17 +448,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         const double Y22 = ROT ? q2 + e2 + a12 * e1 : q2 + e2 + a02 * e0 + a12 * e1;
         const double hx0 = -q0 * rxi + g0, hx1 = -q1 * ryi + g1;
         const double hx2 = ROT ? -q2 * rti + g2 + a12 * g1 : -q2 * rti + g2 + a02 * g0 + a12 * g1;
-        const int ca0 = sti & 3, ca1 = (sti >> 2) & 3;
-        const bool f0 = ca0 == 0, f1 = ca1 == 0;
-        const double bA0 = f0 ? 0.0 : (ca0 == 1 ? lb0 : ub0);
-        const double bA1 = f1 ? 0.0 : (ca1 == 1 ? lb1 : ub1);
-        const double M00 = f0 ? H00 : 1.0, M11 = f1 ? H11 : 1.0, M01 = (f0 && f1) ? H01 : 0.0;
+        // the stage's masked 2 x 2 solve from its code's table entry: M = the free block of H with
+        // ones on the fixed diagonal, S^-1 rows of the fixed inputs zero (exact: products with 0 / 1)
+        const double* tb = btab + 8 * sti;
+        const double bA0 = tb[0], bA1 = tb[1], fm0 = tb[2], om0 = tb[3], fm1 = tb[4], om1 = tb[5];
+        const double fm01 = tb[6];
+        const double M00 = fm0 * H00 + om0, M11 = fm1 * H11 + om1, M01 = fm01 * H01;
         const double det = M00 * M11 - M01 * M01;
         double idet = __builtin_amdgcn_rcp(det);
 #pragma unroll
         for (int nt = 0; nt < F110QP_SEG_NEWTON; nt++) idet = fma(idet, fma(-det, idet, 1.0), idet);
-        const double I00 = f0 ? M11 * idet : 0.0, I11 = f1 ? M00 * idet : 0.0;
-        const double I01 = (f0 && f1) ? -M01 * idet : 0.0;
+        const double I00 = fm0 * (M11 * idet), I11 = fm1 * (M00 * idet);
+        const double I01 = -M01 * idet;
         const double K00 = -I00 * X00 - I01 * X10, K01 = -I00 * X01 - I01 * X11;
         const double K02 = -I00 * X02 - I01 * X12;
         const double K10 = -I01 * X00 - I11 * X10, K11 = -I01 * X01 - I11 * X11;
@@ -660,15 +690,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
                               : r0 * (u0 - ud0) + b00 * l0 + b10 * l1 + b20 * l2;
         const double g1 = r1 * (u1 - ud1) + b21 * l2;
         int st = MODE ? old : 0;
+        const double* tf = ftab + 8 * old;  // (fp64 scratch) the old state's test thresholds
 #pragma unroll
         for (int a = 0; a < 2; a++) {
           const int ca = (old >> (2 * a)) & 3;
           const double u = a ? u1 : u0, g = a ? g1 : g0;
-          const double gta = MODE ? (a ? gtoll1 : gtoll0) : (a ? gtol1 : gtol0);
-          const double lbx = MODE ? (a ? lbl1 : lbl0) : (a ? lbe1 : lbe0);
-          const double ubx = MODE ? (a ? ubl1 : ubl0) : (a ? ube1 : ube0);
-          const bool nlo = ((ca == 1) & (g > -gta)) | ((ca == 0) & (u < lbx));
-          const bool nhi = !nlo & (((ca == 2) & (g < gta)) | ((ca == 0) & (u > ubx)));
+          bool nlo, nhi;
+          if constexpr (!F32) {
+            nlo = (u < tf[4 * a]) | (g > tf[4 * a + 2]);
+            nhi = !nlo & ((u > tf[4 * a + 1]) | (g < tf[4 * a + 3]));
+          } else {
+            const double gta = MODE ? (a ? gtoll1 : gtoll0) : (a ? gtol1 : gtol0);
+            const double lbx = MODE ? (a ? lbl1 : lbl0) : (a ? lbe1 : lbe0);
+            const double ubx = MODE ? (a ? ubl1 : ubl0) : (a ? ube1 : ube0);
+            nlo = ((ca == 1) & (g > -gta)) | ((ca == 0) & (u < lbx));
+            nhi = !nlo & (((ca == 2) & (g < gta)) | ((ca == 0) & (u > ubx)));
+          }
           const int nca = (int)nlo | ((int)nhi << 1);
           if constexpr (MODE == 0) {
             st |= nca << (2 * a);
