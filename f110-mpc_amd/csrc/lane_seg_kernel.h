@@ -293,9 +293,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       r64[(3 * t + 2) * 64] = (double)ft - th0;
     }
     // the active-state code tables: code c holds input a's state (c >> 2a) & 3 (0 free, 1 lower,
-    // 2 upper). btab[c] = (bA0, bA1, fm0, 1 - fm0, fm1, 1 - fm1, fm0 fm1, 0): the fixed inputs'
+    // 2 upper). btab[c] = (bA0, bA1, fm0, fm1, 1 - fm0, 1 - fm1, fm0 fm1, 0): the fixed inputs'
     // bound values and the free masks of the masked 2 x 2 solve (products with 0 / 1 instead of
-    // ~20 selects per backward stage). ftab[c] = per input (u < t1, u > t2, g > t3, g < t4 tests):
+    // ~20 selects per backward stage; the first four are read a stage ahead). ftab[c] = per input (u < t1, u > t2, g > t3, g < t4 tests):
     // the free input's box with the re-guess tolerance, a bound's multiplier sign test, +-inf
     // where the test does not apply (fp64 scratch: one set of tolerances for both pass kinds)
     if (lane < 16) {
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       double* e = btab + 8 * lane;
       e[0] = cA == 0 ? 0.0 : (cA == 1 ? lb0 : ub0);
       e[1] = cB == 0 ? 0.0 : (cB == 1 ? lb1 : ub1);
-      e[2] = fA; e[3] = 1.0 - fA; e[4] = fB; e[5] = 1.0 - fB; e[6] = fA * fB; e[7] = 0.0;
+      e[2] = fA; e[3] = fB; e[4] = 1.0 - fA; e[5] = 1.0 - fB; e[6] = fA * fB; e[7] = 0.0;
       if constexpr (!F32) {
         const double inf = __builtin_inf();
         double* f = ftab + 8 * lane;
@@ -411,13 +411,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     double G00 = 0.0, G01 = 0.0, G02 = 0.0, G11 = 0.0, G12 = 0.0, G22 = 0.0;  // Gam (symmetric)
     {
       int nst = ap[(m - 1) * 64];
+      // the next stage's code-table entry (bA0, bA1, fm0, fm1), read one stage ahead: the masked
+      // solve needs it right after H, which the previous stage's P already gives
+      double nb0 = btab[8 * nst], nb1 = btab[8 * nst + 1], nf0 = btab[8 * nst + 2], nf1 = btab[8 * nst + 3];
       double rx = r64[(3 * (m - 1) + 0) * 64], ry = r64[(3 * (m - 1) + 1) * 64];
       double rt = r64[(3 * (m - 1) + 2) * 64];
       constexpr int kBwUnroll = F110QP_SEG_BW_UNROLL;
 #pragma unroll kBwUnroll
       for (int t = m - 1; t >= 0; t--) {
         ST* s = sc + t * NV * 64;
-        const int sti = nst;
+        const double bA0 = nb0, bA1 = nb1, fm0 = nf0, fm1 = nf1;
         const int tn = t > 0 ? t - 1 : 0;
         nst = ap[tn * 64];
         const double rxi = rx, ryi = ry, rti = rt;
@@ -450,9 +453,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
         const double hx2 = ROT ? -q2 * rti + g2 + a12 * g1 : -q2 * rti + g2 + a02 * g0 + a12 * g1;
         // the stage's masked 2 x 2 solve from its code's table entry: M = the free block of H with
         // ones on the fixed diagonal, S^-1 rows of the fixed inputs zero (exact: products with 0 / 1)
-        const double* tb = btab + 8 * sti;
-        const double bA0 = tb[0], bA1 = tb[1], fm0 = tb[2], om0 = tb[3], fm1 = tb[4], om1 = tb[5];
-        const double fm01 = tb[6];
+        {
+          const double* tb = btab + 8 * nst;
+          nb0 = tb[0]; nb1 = tb[1]; nf0 = tb[2]; nf1 = tb[3];
+        }
+        const double om0 = 1.0 - fm0, om1 = 1.0 - fm1, fm01 = fm0 * fm1;
         const double M00 = fm0 * H00 + om0, M11 = fm1 * H11 + om1, M01 = fm01 * H01;
         const double det = M00 * M11 - M01 * M01;
         double idet = __builtin_amdgcn_rcp(det);
