@@ -197,25 +197,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   // valid address (clamped) and every store lands (past the staged rows for e >= tot), so the
   // loop has no EXEC-masked region: ~11 instructions per element instead of ~50 (ISA).
   // (Issuing chunk 0 first and the linearisation under its loads measured no gain: C2 23.4 against
-  // 23.1 us, C5 30.9 against 30.4, same box.) Twin starts: row q of the wave is QP (b0 + q) >> 1.
+  // 23.1 us, C5 30.9 against 30.4, same box.) Twin starts: row q of the wave is QP (b0 >> 1) + q.
+  // Twin starts: the two starts of a QP share its row, staged once ([3N][L / 2] QP rows)
+  constexpr int LR = L >> twin;
   {
     float* stg = reinterpret_cast<float*>(lbase + o_sc);
-    const int n3 = 3 * N, S3 = 3 * P.xr_stride, tot = nq * n3;
+    const int nqr = (nq + twin) >> twin;  // QP rows of the wave (b0 is even with twin starts)
+    const int n3 = 3 * N, S3 = 3 * P.xr_stride, tot = nqr * n3;
     const int rb0 = b0 >> twin;
     const float* src = xrg + (size_t)rb0 * S3;
     const int dq = 64 / n3, dc = 64 - dq * n3;
     int q = lane / n3, c = lane - (lane / n3) * n3;
-    const int junk = n3 * L + lane;                  // inside the scratch rows, never read
-    const int last_off = (((b0 + nq - 1) >> twin) - rb0) * S3 + (n3 - 1);  // a valid element
-    constexpr int kChunk = 16;  // C5 and the C4 shard stage 960 floats per wave: one round trip
+    const int junk = n3 * LR + lane;                 // inside the scratch rows, never read
+    const int last_off = (nqr - 1) * S3 + (n3 - 1);  // a valid element
+    // C5 and the C4 shard stage 960 floats per wave, the twin kernels 480: one round trip
+    constexpr int kChunk = TWIN ? 8 : 16;
     for (int e0 = 0; e0 < tot; e0 += kChunk * 64) {
       float vbuf[kChunk];
       int dst[kChunk];
 #pragma unroll
       for (int j = 0; j < kChunk; j++) {
         const bool in = e0 + j * 64 + lane < tot;
-        dst[j] = in ? c * L + q : junk;
-        vbuf[j] = src[in ? (((b0 & twin) + q) >> twin) * S3 + c : last_off];
+        dst[j] = in ? c * LR + q : junk;
+        vbuf[j] = src[in ? q * S3 + c : last_off];
         q += dq;
         c += dc;
         const bool wrap = c >= n3;
@@ -282,10 +286,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
   bool nonfin = false;
   {
     const float* stg = reinterpret_cast<const float*>(lbase + o_sc);
+    const int row = slot >> twin;
     for (int t = 0; t < mM; t++) {
       const int i = s0 + t;
-      const float fx = stg[(3 * i + 0) * L + slot], fy = stg[(3 * i + 1) * L + slot];
-      const float ft = stg[(3 * i + 2) * L + slot];
+      const float fx = stg[(3 * i + 0) * LR + row], fy = stg[(3 * i + 1) * LR + row];
+      const float ft = stg[(3 * i + 2) * LR + row];
       nonfin |= (t < m) & !(isfinite(fx) && isfinite(fy) && isfinite(ft));
       const double dx = (double)fx - X0, dy = (double)fy - Y0;
       r64[(3 * t + 0) * 64] = ROT ? cs * dx + sn * dy : dx;
