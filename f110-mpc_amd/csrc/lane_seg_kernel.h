@@ -99,19 +99,21 @@ __device__ __forceinline__ double seg_up(double v, int lane) {
   static_assert(S == 2 || S == 4 || S == 8, "segments per QP: 2, 4 or 8");
   if constexpr (S == 2) return dpp_d<0xB1>(v);       // quad_perm [1, 0, 3, 2]
   else if constexpr (S == 4) return dpp_d<0x39>(v);  // quad_perm [1, 2, 3, 0]
-  else {  // row_shr:7 for the top lane of the group, row_shl:1 for the others; both moves run on
-          // every lane (a DPP move under a divergent branch reads inactive lanes as invalid)
-    const double a = dpp_d<0x117>(v), b = dpp_d<0x101>(v);
-    return (lane & 7) == 7 ? a : b;
+  else {  // row_shl:1; the top segment's lane takes 0 instead of the ring's wrap: its own
+          // (Phi, psi, Gam) are zero in the segment-end recursion, so what it receives only
+          // matters as a non-finite value (a neighbouring QP's lane), and 0 is what it computes
+          // with anyway (one DPP move and a select per dword instead of two moves and a select)
+    const double b = dpp_d<0x101>(v);
+    return (lane & 7) == 7 ? 0.0 : b;
   }
 }
 template <int S>
 __device__ __forceinline__ double seg_dn(double v, int lane) {
   if constexpr (S == 2) return dpp_d<0xB1>(v);
   else if constexpr (S == 4) return dpp_d<0x93>(v);  // quad_perm [3, 0, 1, 2]
-  else {  // row_shl:7 for segment 0 of the group, row_shr:1 for the others
-    const double a = dpp_d<0x107>(v), b = dpp_d<0x111>(v);
-    return (lane & 7) == 0 ? a : b;
+  else {  // row_shr:1; segment 0 takes 0: the ring hands it the top segment's x_e, which is 0
+    const double b = dpp_d<0x111>(v);
+    return (lane & 7) == 0 ? 0.0 : b;
   }
 }
 
