@@ -302,9 +302,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
     // the active-state code tables: code c holds input a's state (c >> 2a) & 3 (0 free, 1 lower,
     // 2 upper). btab[c] = (bA0, bA1, fm0, fm1, 1 - fm0, 1 - fm1, fm0 fm1, 0): the fixed inputs'
     // bound values and the free masks of the masked 2 x 2 solve (products with 0 / 1 instead of
-    // ~20 selects per backward stage; the first four are read a stage ahead). ftab[c] = per input (u < t1, u > t2, g > t3, g < t4 tests):
-    // the free input's box with the re-guess tolerance, a bound's multiplier sign test, +-inf
-    // where the test does not apply (fp64 scratch: one set of tolerances for both pass kinds)
+    // ~20 selects per backward stage; the first four are read a stage ahead). ftab[c] = per input
+    // the forward sweep's re-guess thresholds and masks (fp64 scratch: one set of tolerances for
+    // both pass kinds)
     if (lane < 16) {
       const int cA = lane & 3, cB = (lane >> 2) & 3;
       const double fA = cA == 0 ? 1.0 : 0.0, fB = cB == 0 ? 1.0 : 0.0;
@@ -313,12 +313,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
       e[1] = cB == 0 ? 0.0 : (cB == 1 ? lb1 : ub1);
       e[2] = fA; e[3] = fB; e[4] = 1.0 - fA; e[5] = 1.0 - fB; e[6] = fA * fB; e[7] = 0.0;
       if constexpr (!F32) {
+        // per input (lo, hi, fm, 1 - fm): the re-guess tests y = fm u - (1 - fm) g against
+        // y < lo (lower) and y > hi (upper); free: y = u in (lbe, ube); at the lower bound: y = -g,
+        // stays while -g < gtol; at the upper: y = -g, stays while -g > -gtol
         const double inf = __builtin_inf();
         double* f = ftab + 8 * lane;
-        f[0] = cA == 0 ? lbe0 : -inf; f[1] = cA == 0 ? ube0 : inf;
-        f[2] = cA == 1 ? -gtol0 : inf; f[3] = cA == 2 ? gtol0 : -inf;
-        f[4] = cB == 0 ? lbe1 : -inf; f[5] = cB == 0 ? ube1 : inf;
-        f[6] = cB == 1 ? -gtol1 : inf; f[7] = cB == 2 ? gtol1 : -inf;
+        f[0] = cA == 0 ? lbe0 : (cA == 1 ? gtol0 : -inf); f[1] = cA == 0 ? ube0 : (cA == 2 ? -gtol0 : inf);
+        f[2] = fA; f[3] = 1.0 - fA;
+        f[4] = cB == 0 ? lbe1 : (cB == 1 ? gtol1 : -inf); f[5] = cB == 0 ? ube1 : (cB == 2 ? -gtol1 : inf);
+        f[6] = fB; f[7] = 1.0 - fB;
       }
     }
     __syncthreads();  // the staging region becomes the Riccati scratch
@@ -709,8 +712,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(F110QP_SEG_W
           const double u = a ? u1 : u0, g = a ? g1 : g0;
           bool nlo, nhi;
           if constexpr (!F32) {
-            nlo = (u < tf[4 * a]) | (g > tf[4 * a + 2]);
-            nhi = !nlo & ((u > tf[4 * a + 1]) | (g < tf[4 * a + 3]));
+            // (the two tests exclude each other: lbe < ube, and a bound input has one test)
+            const double y = tf[4 * a + 2] * u - tf[4 * a + 3] * g;
+            nlo = y < tf[4 * a];
+            nhi = y > tf[4 * a + 1];
           } else {
             const double gta = MODE ? (a ? gtoll1 : gtoll0) : (a ? gtol1 : gtol0);
             const double lbx = MODE ? (a ? lbl1 : lbl0) : (a ? lbe1 : lbe0);
